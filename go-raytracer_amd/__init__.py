@@ -1,0 +1,13 @@
+"""MI355X-native renderer for the ICFP-2000 GML raytracer hot path.
+
+Layout:
+  csrc/rt_kernel.hip   HIP megakernel (gfx950) + the C ABI of include/rt_abi.h
+  abi.py               ctypes mirror of include/rt_abi.h
+  scene.py             host scene values, BFS flattening, surface baking
+  gomath.py            Go float64 host math (transform matrices)
+  configs.py           canned.gml and the BASELINE configs C1..C5
+  render.py            Render(): the reference's entry point over the C ABI
+  dist.py              row-band sharding across GPUs + RCCL gather
+"""
+from . import abi, configs, gomath, scene  # noqa: F401
+from .render import Render, RenderContext, load_library  # noqa: F401

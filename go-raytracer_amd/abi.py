@@ -1,0 +1,130 @@
+"""ctypes mirror of include/rt_abi.h (the C ABI of the renderer).
+
+Struct layouts must match include/rt_abi.h exactly; tests/test_abi.py checks
+sizes and offsets against the compiled library's expectations.
+"""
+import ctypes as C
+
+RT_OK = 0
+RT_E_INVALID = -1
+RT_E_SINGULAR = -2
+RT_E_DEVICE = -3
+RT_E_NOMEM = -4
+
+RT_SPHERE, RT_PLANE, RT_CUBE, RT_CYLINDER = 0, 1, 2, 3
+RT_NUM_KINDS = 4
+RT_MAX_FACES = 6
+KIND_NAMES = ("sphere", "plane", "cube", "cylinder")
+
+
+class rt_material(C.Structure):
+    _fields_ = [
+        ("color", C.c_double * 3),
+        ("reflectivity", C.c_double),
+        ("fuzziness", C.c_double),
+        ("transparency", C.c_double),
+        ("refractive_index", C.c_double),
+        ("kd", C.c_double),
+        ("ks", C.c_double),
+        ("specular_exponent", C.c_double),
+    ]
+
+
+class rt_point_light(C.Structure):
+    _fields_ = [("position", C.c_double * 3), ("color", C.c_double * 3)]
+
+
+class rt_object(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("has_transform", C.c_int32),
+        ("material", C.c_int32 * RT_MAX_FACES),
+        ("transform", C.c_double * 16),
+        ("plane_point", C.c_double * 3),
+        ("plane_normal", C.c_double * 3),
+    ]
+
+
+class rt_scene(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("depth", C.c_int32),
+        ("num_lights", C.c_int32),
+        ("fov", C.c_double),
+        ("ambient", C.c_double * 3),
+        ("bg_start", C.c_double * 3),
+        ("bg_end", C.c_double * 3),
+        ("lights", C.POINTER(rt_point_light)),
+        ("objects", C.POINTER(rt_object)),
+        ("materials", C.POINTER(rt_material)),
+        ("num_objects", C.c_int32),
+        ("num_materials", C.c_int32),
+    ]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [
+        ("primary_rays", C.c_uint64),
+        ("secondary_rays", C.c_uint64),
+        ("shadow_rays", C.c_uint64),
+        ("tests", C.c_uint64 * RT_NUM_KINDS),
+        ("shadow_tests", C.c_uint64 * RT_NUM_KINDS),
+        ("shaded_hits", C.c_uint64),
+        ("kernel_ms", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {
+            "primary_rays": int(self.primary_rays),
+            "secondary_rays": int(self.secondary_rays),
+            "shadow_rays": int(self.shadow_rays),
+            "tests": [int(v) for v in self.tests],
+            "shadow_tests": [int(v) for v in self.shadow_tests],
+            "shaded_hits": int(self.shaded_hits),
+        }
+
+    def total_rays(self):
+        return int(self.primary_rays) + int(self.secondary_rays) + int(self.shadow_rays)
+
+
+class PackedScene:
+    """Owns the ctypes arrays an rt_scene points into (keeps them alive)."""
+
+    def __init__(self, scene, lights, objects, materials):
+        self.scene = scene
+        self._lights = lights
+        self._objects = objects
+        self._materials = materials
+
+    @property
+    def width(self):
+        return int(self.scene.width)
+
+    @property
+    def height(self):
+        return int(self.scene.height)
+
+    def ref(self):
+        return C.byref(self.scene)
+
+
+# Algorithmic FP64 flops per Intersect call, by kind (SURVEY.md §8(d):
+# +,-,*,/,sqrt = 1 each, compares 0; miss-path counts, i.e. a lower bound).
+# sphere: 33 (ray->object) + 19 (a, halfB, c, discriminant) = 52
+# plane : 33 + 5 (denom) + 7 (numerator) ... = 45 on the non-parallel path
+# cube  : 6 planes = 270 (the reference re-transforms the ray per face)
+# cylinder: 33 + ~51 = 84
+FLOPS_PER_TEST = (52, 45, 270, 84)
+# Per shaded hit: surface props + ambient (21); per light: lighting (68).
+FLOPS_PER_SHADE = 21
+FLOPS_PER_LIGHT = 68
+
+
+def algorithmic_flops(stats, num_lights):
+    """Sum of count x flops over the work the render did (lower bound)."""
+    f = 0
+    for k in range(RT_NUM_KINDS):
+        f += (int(stats.tests[k]) + int(stats.shadow_tests[k])) * FLOPS_PER_TEST[k]
+    f += int(stats.shaded_hits) * (FLOPS_PER_SHADE + FLOPS_PER_LIGHT * num_lights)
+    return f

@@ -1,0 +1,131 @@
+"""Scenes the path is measured and parity-tested on.
+
+- canned(): internal/gml/testdata/canned.gml (golden testdata/goldens/
+  example_canned.png), built with the same transform composition the GML
+  evaluator performs (evaluator.go:176-184, union :1064-1075).
+- C1..C5: the BASELINE.json configs as concrete synthetic scenes (SURVEY.md
+  §8(d)). All surfaces are constant materials. Where a config names a feature
+  the reference does not render (cone, CSG difference), the parity-graded
+  substitute of SURVEY.md §8(d) is used and the name says so.
+"""
+from . import scene as S
+
+BG0 = (0.0, 0.0, 0.0)
+BG1 = (0.5, 0.7, 1.0)
+WHITE = (1.0, 1.0, 1.0)
+
+
+def canned(width=1900, height=1200):
+    """canned.gml:1-96 (1900x1200, depth 7, fov 120, gradient background)."""
+    glass = S.Sphere(S.material((0.8, 0.2, 0.2), 0.0, 0.0, 0.9, 1.5, 1.0, 0.8, 50.0)).translate(0.0, 0.0, 5.0)
+    dull = S.Sphere(S.material((0.2, 0.2, 0.8), 0.2, 0.5, 0.0, 0.0, 1.0, 0.0, 0.0)).translate(2.0, 0.0, 8.0)
+    green = S.Sphere(S.material((0.2, 0.8, 0.2), 0.8, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0)).translate(-2.0, 0.0, 6.0)
+    ground = S.Sphere(S.surface((0.8, 0.8, 0.8), 1.0, 0.0, 0.0)).translate(0.0, -1001.0, 5.0).uscale(1000.0)
+    sc = S.union(S.union(S.union(ground, glass), dull), green)
+    light = S.PointLight((5.0, 5.0, 0.0), WHITE)
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=[light], scene=sc, depth=7, fov=120.0,
+                        width=width, height=height, file="canned.ppm", bg_start=BG0, bg_end=BG1)
+
+
+def c1(width=256, height=256):
+    """C1: one unit sphere at (0,0,3), `0.8 0.2 0.2 point 1.0 0.2 1.0` surface, light
+    (-10,10,0), ambient 0.5, 256x256, depth 1 (the sphere.gml shape with a constant
+    surface; plumbing config)."""
+    s = S.Sphere(S.surface((0.8, 0.2, 0.2), 1.0, 0.2, 1.0)).translate(0.0, 0.0, 3.0)
+    light = S.PointLight((-10.0, 10.0, 0.0), WHITE)
+    return S.RenderArgs(ambient=(0.5, 0.5, 0.5), lights=[light], scene=s, depth=1, fov=90.0,
+                        width=width, height=height, file="c1.ppm", bg_start=BG0, bg_end=BG1)
+
+
+def c2(width=1920, height=1080):
+    """C2: the canned spheres (mirror, fuzzy, glass) + plane y=-1; lights (5,5,0),
+    (-5,5,2); ambient 0.1; 1920x1080; depth 4."""
+    mirror = S.Sphere(S.material((0.2, 0.8, 0.2), 0.8, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0)).translate(-2.0, 0.0, 6.0)
+    fuzzy = S.Sphere(S.material((0.2, 0.2, 0.8), 0.2, 0.5, 0.0, 0.0, 1.0, 0.0, 0.0)).translate(2.0, 0.0, 8.0)
+    glass = S.Sphere(S.material((0.8, 0.2, 0.2), 0.0, 0.0, 0.9, 1.5, 1.0, 0.8, 50.0)).translate(0.0, 0.0, 5.0)
+    ground = S.Plane(S.surface((0.8, 0.8, 0.8), 1.0, 0.0, 0.0)).translate(0.0, -1.0, 0.0)
+    sc = S.union(S.union(S.union(ground, glass), fuzzy), mirror)
+    lights = [S.PointLight((5.0, 5.0, 0.0), WHITE), S.PointLight((-5.0, 5.0, 2.0), WHITE)]
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=sc, depth=4, fov=90.0,
+                        width=width, height=height, file="c2.ppm", bg_start=BG0, bg_end=BG1)
+
+
+def c3(width=3840, height=2160):
+    """C3 (bench workload): ICFP tier-2 primitives -- cylinder + cube + (sphere in
+    place of the cone the reference lacks) over a reflective
+    ground plane; 4 lights at (+-5,5,0), (+-5,5,10); 3840x2160; depth 6.
+    The glass cylinder is both reflective and transparent, so rays branch."""
+    glass_cyl = (S.Cylinder(S.material((0.9, 0.9, 1.0), 0.3, 0.0, 0.7, 1.4, 0.6, 0.9, 40.0))
+                 .translate(-1.2, -1.0, 5.5).scale(0.8, 1.8, 0.8))
+    mirror_cube = (S.Cube(S.material((0.8, 0.7, 0.3), 0.6, 0.05, 0.0, 0.0, 0.8, 0.5, 20.0))
+                   .translate(1.4, -1.0, 6.5).rotatey(35.0).rotatex(10.0).uscale(1.3).translate(-0.5, 0.0, -0.5))
+    ball = (S.Sphere(S.material((0.2, 0.6, 0.9), 0.1, 0.0, 0.0, 0.0, 0.9, 0.6, 30.0))
+            .translate(0.3, -0.35, 3.8).uscale(0.65))
+    ground = S.Plane(S.material((0.7, 0.7, 0.7), 0.35, 0.0, 0.0, 0.0, 1.0, 0.1, 5.0)).translate(0.0, -1.0, 0.0)
+    sc = S.union(S.union(S.union(ground, glass_cyl), mirror_cube), ball)
+    lights = [S.PointLight((5.0, 5.0, 0.0), (0.6, 0.6, 0.6)), S.PointLight((-5.0, 5.0, 0.0), (0.6, 0.6, 0.6)),
+              S.PointLight((5.0, 5.0, 10.0), (0.5, 0.5, 0.5)), S.PointLight((-5.0, 5.0, 10.0), (0.5, 0.5, 0.5))]
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=sc, depth=6, fov=90.0,
+                        width=width, height=height, file="c3.ppm", bg_start=BG0, bg_end=BG1)
+
+
+def c4(width=3840, height=2160):
+    """C4 parity-graded substitute: cube U 64 spheres (r 0.1) on a 4x4x4 lattice --
+    the reference does not render CSG difference (raytracer.go:825-826); 3840x2160,
+    depth 8."""
+    cube = (S.Cube(S.material((0.9, 0.3, 0.3), 0.2, 0.0, 0.0, 0.0, 0.9, 0.4, 10.0))
+            .translate(-0.1, -0.6, 5.0).rotatey(30.0).rotatex(20.0).uscale(1.6).translate(-0.5, -0.5, -0.5))
+    glass = S.material((0.9, 1.0, 0.9), 0.2, 0.0, 0.8, 1.5, 0.5, 0.8, 60.0)
+    chrome = S.material((0.9, 0.9, 0.9), 0.7, 0.0, 0.0, 0.0, 0.5, 0.8, 60.0)
+    sc = cube
+    for i in range(4):
+        for j in range(4):
+            for k in range(4):
+                m = glass if (i + j + k) % 2 == 0 else chrome
+                sph = (S.Sphere(m).translate(-0.1 + (i - 1.5) * 0.55, -0.6 + (j - 1.5) * 0.55, 5.0 + (k - 1.5) * 0.55)
+                       .uscale(0.1))
+                sc = S.union(sc, sph)
+    ground = S.Plane(S.material((0.6, 0.6, 0.7), 0.3, 0.0, 0.0, 0.0, 1.0, 0.0, 1.0)).translate(0.0, -2.0, 0.0)
+    sc = S.union(sc, ground)
+    lights = [S.PointLight((4.0, 6.0, 0.0), (0.8, 0.8, 0.8)), S.PointLight((-6.0, 4.0, 2.0), (0.5, 0.5, 0.6))]
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=sc, depth=8, fov=90.0,
+                        width=width, height=height, file="c4.ppm", bg_start=BG0, bg_end=BG1)
+
+
+class _Pcg32:
+    """Tiny deterministic generator for scene jitter (seed 2026); not on the path."""
+
+    def __init__(self, seed):
+        self.state = (seed * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
+
+    def uniform(self):
+        self.state = (self.state * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
+        x = self.state >> 11
+        return x / float(1 << 53)
+
+
+def c5(width=7680, height=4320, nx=100, ny=100, nz=10):
+    """C5: 100 000 spheres on a jittered 100x100x10 lattice in z in [4,14], uscale 0.04,
+    every 4th reflective 0.5, + ground plane; 2 lights; 7680x4320; depth 8."""
+    rng = _Pcg32(2026)
+    matte = S.material((0.8, 0.5, 0.3), 0.0, 0.0, 0.0, 0.0, 0.9, 0.3, 8.0)
+    shiny = S.material((0.6, 0.7, 0.9), 0.5, 0.0, 0.0, 0.0, 0.7, 0.6, 30.0)
+    objs = []
+    n = 0
+    for k in range(nz):
+        for j in range(ny):
+            for i in range(nx):
+                x = -4.0 + 8.0 * (i + 0.5) / nx + (rng.uniform() - 0.5) * 0.03
+                y = -2.5 + 5.0 * (j + 0.5) / ny + (rng.uniform() - 0.5) * 0.03
+                z = 4.0 + 10.0 * (k + 0.5) / nz + (rng.uniform() - 0.5) * 0.2
+                m = shiny if n % 4 == 0 else matte
+                objs.append(S.Sphere(m).translate(x, y, z).uscale(0.04))
+                n += 1
+    ground = S.Plane(S.material((0.5, 0.5, 0.5), 0.2, 0.0, 0.0, 0.0, 1.0, 0.0, 1.0)).translate(0.0, -3.0, 0.0)
+    sc = S.Union(tuple(objs) + (ground,))
+    lights = [S.PointLight((6.0, 8.0, -2.0), (0.8, 0.8, 0.8)), S.PointLight((-6.0, 6.0, 0.0), (0.5, 0.5, 0.5))]
+    return S.RenderArgs(ambient=(0.15, 0.15, 0.15), lights=lights, scene=sc, depth=8, fov=90.0,
+                        width=width, height=height, file="c5.ppm", bg_start=BG0, bg_end=BG1)
+
+
+CONFIGS = {"canned": canned, "c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}

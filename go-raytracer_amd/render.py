@@ -1,0 +1,146 @@
+"""Render(): the reference's entry point (raytracer.go:589) over the C ABI.
+
+The only compute path is the HIP library csrc/librtamd.so (gfx950). There is
+no CPU fallback: if the library or a HIP device is missing, every call raises.
+PyTorch is used only for device memory and streams.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from . import scene as _scene
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "csrc", "librtamd.so")
+
+_lib = None
+
+
+class RenderError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    """Load librtamd.so and declare the include/rt_abi.h signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RenderError("HIP renderer library not built: %s (run __graft_entry__.build())" % path)
+    l = C.CDLL(path)
+    vp, i = C.c_void_p, C.c_int
+    l.rt_abi_version.argtypes = []
+    l.rt_abi_version.restype = i
+    l.rt_last_error.argtypes = []
+    l.rt_last_error.restype = C.c_char_p
+    l.rt_create.argtypes = [i, C.POINTER(vp)]
+    l.rt_create.restype = i
+    l.rt_destroy.argtypes = [vp]
+    l.rt_destroy.restype = None
+    l.rt_set_scene.argtypes = [vp, vp]
+    l.rt_set_scene.restype = i
+    l.rt_render_rows_async.argtypes = [vp, i, i, vp, vp]
+    l.rt_render_rows_async.restype = i
+    l.rt_read_stats.argtypes = [vp, vp, i, vp]
+    l.rt_read_stats.restype = i
+    l.rt_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    l.rt_last_kernel_ms.restype = i
+    l.rt_render.argtypes = [vp, vp, vp]
+    l.rt_render.restype = i
+    if l.rt_abi_version() != 1:
+        raise RenderError("librtamd ABI version mismatch")
+    _lib = l
+    return l
+
+
+def _check(rc, what):
+    if rc != abi.RT_OK:
+        msg = _lib.rt_last_error() if _lib is not None else b""
+        raise RenderError("%s failed (%d): %s" % (what, rc, (msg or b"").decode(errors="replace")))
+
+
+def _packed(scene_or_args):
+    if isinstance(scene_or_args, abi.PackedScene):
+        return scene_or_args
+    return _scene.convert(scene_or_args)
+
+
+class RenderContext:
+    """One device context: scene resident in HBM, renders rows on a torch stream."""
+
+    def __init__(self, device=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RenderError("no HIP device visible: the renderer has no CPU path")
+        self.torch = torch
+        self.lib = load_library()
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        with torch.cuda.device(self.device):
+            h = C.c_void_p()
+            _check(self.lib.rt_create(self.device, C.byref(h)), "rt_create")
+        self.handle = h
+        self.packed = None
+
+    def close(self):
+        if self.handle:
+            self.lib.rt_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, scene_or_args):
+        self.packed = _packed(scene_or_args)
+        _check(self.lib.rt_set_scene(self.handle, self.packed.ref()), "rt_set_scene")
+        return self.packed
+
+    def render_rows_async(self, y0, y1, out, stream=None):
+        """Enqueue rows [y0, y1) into the uint8 CUDA tensor `out` ([y1-y0, W, 4])."""
+        torch = self.torch
+        W = self.packed.width
+        assert out.dtype == torch.uint8 and out.is_cuda and out.is_contiguous()
+        assert out.numel() == (y1 - y0) * W * 4, "output tensor shape does not match rows"
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
+        _check(self.lib.rt_render_rows_async(self.handle, int(y0), int(y1), C.c_void_p(out.data_ptr()),
+                                             C.c_void_p(s.cuda_stream)), "rt_render_rows_async")
+
+    def read_stats(self, reset=True, stream=None):
+        s = self.torch.cuda.current_stream(self.device) if stream is None else stream
+        st = abi.rt_stats()
+        _check(self.lib.rt_read_stats(self.handle, C.c_void_p(s.cuda_stream), int(reset), C.byref(st)),
+               "rt_read_stats")
+        return st
+
+    def last_kernel_ms(self):
+        ms = C.c_double()
+        _check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)), "rt_last_kernel_ms")
+        return ms.value
+
+    def render(self, y0=0, y1=None):
+        """Synchronous render of rows [y0, y1) -> numpy uint8 [rows, W, 4]."""
+        torch = self.torch
+        if y1 is None:
+            y1 = self.packed.height
+        out = torch.empty((y1 - y0, self.packed.width, 4), dtype=torch.uint8, device="cuda:%d" % self.device)
+        self.render_rows_async(y0, y1, out)
+        torch.cuda.synchronize(self.device)
+        return out.cpu().numpy()
+
+
+def Render(scene_or_args, return_stats=False):
+    """Render(scene) -> RGBA8 image as numpy [H, W, 4] (Go image.RGBA.Pix layout),
+    raytracer.go:589-682. Runs on the current HIP device."""
+    ctx = RenderContext()
+    try:
+        ctx.set_scene(scene_or_args)
+        ctx.read_stats(reset=True)
+        img = ctx.render()
+        st = ctx.read_stats(reset=True)
+    finally:
+        ctx.close()
+    return (img, st) if return_stats else img

@@ -1,0 +1,253 @@
+"""Host-side scene values and the flattening into the C ABI (rt_scene).
+
+Mirrors the reference's GML scene-object values (internal/gml/evaluator.go:
+157-292) and the union flattening / surface baking that sits in front of the
+render hot path (raytracer.go:724-830), so a caller holding a gml.RenderArgs
+equivalent gets exactly the object order and matrices the reference renders.
+
+Everything here is host plumbing executed once per frame; the per-pixel work
+happens in the HIP kernel behind include/rt_abi.h.
+"""
+import ctypes as C
+from dataclasses import dataclass, field, replace
+from typing import List, Optional
+
+from . import abi
+from . import gomath
+
+
+@dataclass(frozen=True)
+class Material:
+    """gml.Material (evaluator.go:136-150)."""
+    color: tuple = (0.0, 0.0, 0.0)
+    reflectivity: float = 0.0
+    fuzziness: float = 0.0
+    transparency: float = 0.0
+    refractive_index: float = 0.0
+    kd: float = 0.0
+    ks: float = 0.0
+    specular_exponent: float = 0.0
+
+
+def material(color, refl, fuzz, transparency, refr, kd, ks, n):
+    """The `material` builtin's argument order: color refl fuzz transparency refr kd ks n
+    (evaluator.go:869-893)."""
+    return Material(tuple(float(c) for c in color), float(refl), float(fuzz), float(transparency),
+                    float(refr), float(kd), float(ks), float(n))
+
+
+def surface(color, kd, ks, n):
+    """A surface function returning the contest's `color kd ks n`: EvalSurfaceFn maps
+    it to a Material with Reflectivity = ks (evaluator.go:700-726)."""
+    return Material(color=tuple(float(c) for c in color), kd=float(kd), ks=float(ks),
+                    specular_exponent=float(n), reflectivity=float(ks))
+
+
+@dataclass(frozen=True)
+class PointLight:
+    """gml.PointLight (evaluator.go:289-292)."""
+    position: tuple
+    color: tuple
+
+
+class SceneObject:
+    """gml.SceneObject (evaluator.go:152-156): Transform composes existing.MulMat(new)."""
+
+    transform_mat = None
+
+    def transform(self, mat):
+        new = mat if self.transform_mat is None else gomath.mul_mat(self.transform_mat, mat)
+        return replace(self, transform_mat=new)
+
+    # GML builtins on scene objects (evaluator.go:1015-1062)
+    def translate(self, x, y, z):
+        return self.transform(gomath.translate(float(x), float(y), float(z)))
+
+    def scale(self, x, y, z):
+        return self.transform(gomath.scale(float(x), float(y), float(z)))
+
+    def uscale(self, s):
+        s = float(s)
+        return self.transform(gomath.scale(s, s, s))
+
+    def rotatex(self, deg):
+        return self.transform(gomath.rotate_x(gomath.deg_to_rad(float(deg))))
+
+    def rotatey(self, deg):
+        return self.transform(gomath.rotate_y(gomath.deg_to_rad(float(deg))))
+
+    def rotatez(self, deg):
+        return self.transform(gomath.rotate_z(gomath.deg_to_rad(float(deg))))
+
+
+@dataclass(frozen=True)
+class Sphere(SceneObject):
+    """Unit sphere at the origin (evaluator.go:157-175, builtin :755-770).
+    `surface` is a Material or a per-face tuple of Materials (face 0 only)."""
+    surface: object = Material()
+    transform_mat: Optional[list] = None
+
+
+@dataclass(frozen=True)
+class Cube(SceneObject):
+    """Unit cube [0,1]^3 (evaluator.go:185-204). Per-face surface: 6-tuple
+    indexed by prim.CubeSide (internal/prim/plane.go:14-25)."""
+    surface: object = Material()
+    transform_mat: Optional[list] = None
+
+
+@dataclass(frozen=True)
+class Cylinder(SceneObject):
+    """Unit cylinder x^2+z^2<=1, 0<=y<=1 (evaluator.go:206-223). Per-face surface:
+    (side, top, bottom) (raytracer.go:263-267)."""
+    surface: object = Material()
+    transform_mat: Optional[list] = None
+
+
+@dataclass(frozen=True)
+class Plane(SceneObject):
+    """Plane through point with normal (builtin: (0,0,0), (0,1,0), evaluator.go:813-821)."""
+    surface: object = Material()
+    transform_mat: Optional[list] = None
+    point: tuple = (0.0, 0.0, 0.0)
+    normal: tuple = (0.0, 1.0, 0.0)
+
+
+@dataclass(frozen=True)
+class Union(SceneObject):
+    """gml.Union (evaluator.go:244-262). Transform distributes over members."""
+    objects: tuple = ()
+
+    def transform(self, mat):
+        return Union(tuple(o.transform(mat) for o in self.objects))
+
+
+def union(first, second):
+    """The `union` builtin: `first second union` pops second then first and builds
+    Union{Objects: [second, first]} (evaluator.go:1064-1075)."""
+    return Union((second, first))
+
+
+@dataclass(frozen=True)
+class Difference(SceneObject):
+    """gml.Difference (evaluator.go:264-287). The reference renderer rejects it
+    (raytracer.go:825-826) and so does convert()."""
+    a: object = None
+    b: object = None
+
+    def transform(self, mat):
+        return Difference(self.a.transform(mat), self.b.transform(mat))
+
+
+@dataclass
+class RenderArgs:
+    """gml.RenderArgs (evaluator.go:14-28)."""
+    ambient: tuple
+    lights: List[PointLight]
+    scene: SceneObject
+    depth: int
+    fov: float
+    width: int
+    height: int
+    file: str = "out.ppm"
+    bg_start: tuple = (0.0, 0.0, 0.0)
+    bg_end: tuple = (0.0, 0.0, 0.0)
+
+
+_NFACES = {abi.RT_SPHERE: 1, abi.RT_PLANE: 1, abi.RT_CUBE: 6, abi.RT_CYLINDER: 3}
+_KIND = {Sphere: abi.RT_SPHERE, Plane: abi.RT_PLANE, Cube: abi.RT_CUBE, Cylinder: abi.RT_CYLINDER}
+
+
+def flatten(root):
+    """BFS union flattening, raytracer.go:776-828 (order decides closestHit ties)."""
+    out = []
+    queue = [root]
+    while queue:
+        obj = queue.pop(0)
+        if isinstance(obj, Union):
+            queue.extend(obj.objects)
+        elif type(obj) in _KIND:
+            out.append(obj)
+        else:
+            raise TypeError("unknown scene object type %s" % type(obj).__name__)
+    return out
+
+
+def _face_materials(obj, kind):
+    s = obj.surface
+    n = _NFACES[kind]
+    if isinstance(s, Material):
+        return [s] * n
+    s = tuple(s)
+    if len(s) != n:
+        raise ValueError("%s needs %d per-face surfaces, got %d" % (type(obj).__name__, n, len(s)))
+    return list(s)
+
+
+def convert(args: RenderArgs) -> abi.PackedScene:
+    """Flatten RenderArgs into the rt_scene the C ABI takes."""
+    objs = flatten(args.scene)
+    mats: List[Material] = []
+    mat_index = {}
+
+    def midx(m):
+        if m not in mat_index:
+            mat_index[m] = len(mats)
+            mats.append(m)
+        return mat_index[m]
+
+    c_objs = (abi.rt_object * max(1, len(objs)))()
+    for i, o in enumerate(objs):
+        kind = _KIND[type(o)]
+        co = c_objs[i]
+        co.kind = kind
+        fm = _face_materials(o, kind)
+        idx = [midx(m) for m in fm]
+        for f in range(abi.RT_MAX_FACES):
+            co.material[f] = idx[f] if f < len(idx) else idx[0]
+        if o.transform_mat is not None:
+            co.has_transform = 1
+            for r in range(4):
+                for c in range(4):
+                    co.transform[r * 4 + c] = float(o.transform_mat[r][c])
+        else:
+            co.has_transform = 0
+        if kind == abi.RT_PLANE:
+            for k in range(3):
+                co.plane_point[k] = float(o.point[k])
+                co.plane_normal[k] = float(o.normal[k])
+    if not mats:
+        mats.append(Material())
+    c_mats = (abi.rt_material * len(mats))()
+    for i, m in enumerate(mats):
+        cm = c_mats[i]
+        for k in range(3):
+            cm.color[k] = float(m.color[k])
+        cm.reflectivity = m.reflectivity
+        cm.fuzziness = m.fuzziness
+        cm.transparency = m.transparency
+        cm.refractive_index = m.refractive_index
+        cm.kd = m.kd
+        cm.ks = m.ks
+        cm.specular_exponent = m.specular_exponent
+    c_lights = (abi.rt_point_light * max(1, len(args.lights)))()
+    for i, l in enumerate(args.lights):
+        for k in range(3):
+            c_lights[i].position[k] = float(l.position[k])
+            c_lights[i].color[k] = float(l.color[k])
+    sc = abi.rt_scene()
+    sc.width = int(args.width)
+    sc.height = int(args.height)
+    sc.depth = int(args.depth)
+    sc.num_lights = len(args.lights)
+    sc.fov = float(args.fov)
+    for k in range(3):
+        sc.ambient[k] = float(args.ambient[k])
+        sc.bg_start[k] = float(args.bg_start[k])
+        sc.bg_end[k] = float(args.bg_end[k])
+    sc.lights = C.cast(c_lights, C.POINTER(abi.rt_point_light))
+    sc.objects = C.cast(c_objs, C.POINTER(abi.rt_object))
+    sc.materials = C.cast(c_mats, C.POINTER(abi.rt_material))
+    sc.num_objects = len(objs)
+    sc.num_materials = len(mats)
+    return abi.PackedScene(sc, c_lights, c_objs, c_mats)

@@ -1,0 +1,179 @@
+/*
+ * rt_abi.h -- C ABI of the MI355X-native renderer for the ICFP-2000 GML
+ * raytracer (drop-in for the per-pixel Render() hot path of
+ * timdestan/go-raytracer).
+ *
+ * What this replaces (reference file:line, relative to the reference repo):
+ *   - raytracer.go:589-682   func Render(scene *Scene) image.Image
+ *   - raytracer.go:724-830   ConvertRenderArgsToScene / convertGMLSceneObjects
+ *                            (matrix inverse, normal matrices, plane D and
+ *                            NormalWorld, cube face expansion) -- done inside
+ *                            the library from the flattened object list below
+ *   - raytracer.go:38-370    the SceneObject plug-in (Sphere/Plane/Cube/Cylinder
+ *                            Intersect + ComputeSurfaceProps)
+ *   - raytracer.go:372-562   computeLighting / inShadow / refract / fresnel /
+ *                            closestHit / traceRay
+ * The GML interpreter (internal/gml) stays on the host: it produces
+ * gml.RenderArgs (evaluator.go:14-28); the host flattens RenderArgs.Scene in
+ * the same BFS order as raytracer.go:776-828 and bakes each object's surface
+ * into per-face constant materials (gml.Material, evaluator.go:136-150).
+ *
+ * Conventions: plain C, no exceptions cross this boundary; every entry point
+ * returns RT_OK (0) or a negative RT_E* code, and rt_last_error() gives a
+ * thread-local message. The output framebuffer has the exact layout of Go's
+ * image.RGBA.Pix (row-major RGBA8, stride 4*width, alpha 255), so a cgo shim
+ * can wrap it without copying.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* Status codes. */
+#define RT_OK 0
+#define RT_E_INVALID (-1)   /* bad argument / malformed scene             */
+#define RT_E_SINGULAR (-2)  /* transform has det == 0 (prim/vec.go:343)   */
+#define RT_E_DEVICE (-3)    /* HIP runtime error                          */
+#define RT_E_NOMEM (-4)     /* device allocation failed                   */
+
+/* Primitive kinds (the concrete SceneObject types, raytracer.go:43-277). */
+#define RT_SPHERE 0
+#define RT_PLANE 1
+#define RT_CUBE 2
+#define RT_CYLINDER 3
+#define RT_NUM_KINDS 4
+
+#define RT_MAX_FACES 6 /* prim.NUM_CUBE_SIDES, internal/prim/plane.go:27 */
+
+/* gml.Material (internal/gml/evaluator.go:136-150), field for field. */
+typedef struct rt_material {
+    double color[3];
+    double reflectivity;
+    double fuzziness;
+    double transparency;
+    double refractive_index;
+    double kd;
+    double ks;
+    double specular_exponent;
+} rt_material;
+
+/* gml.PointLight (internal/gml/evaluator.go:289-292). */
+typedef struct rt_point_light {
+    double position[3];
+    double color[3];
+} rt_point_light;
+
+/* One flattened scene object (a leaf of gml.RenderArgs.Scene after the BFS
+ * union flattening of raytracer.go:776-828).
+ *   transform      gml.<Kind>.TransformMat, row-major prim.Mat4
+ *                  (object -> world); ignored when has_transform == 0 (nil
+ *                  TransformMat => identity, raytracer.go:757-762).
+ *   material[f]    index into rt_scene.materials for face f (the value
+ *                  EvalSurfaceFn returns for that face; constant surfaces use
+ *                  the same index for every face). Faces: sphere/plane 0;
+ *                  cylinder 0 side, 1 top, 2 bottom (raytracer.go:263-267);
+ *                  cube 0..5 = prim.CubeSide (internal/prim/plane.go:14-25).
+ *   plane_point,
+ *   plane_normal   RT_PLANE only: gml.Plane.Plane (evaluator.go:813-821 builds
+ *                  point (0,0,0), normal (0,1,0)). */
+typedef struct rt_object {
+    int32_t kind;
+    int32_t has_transform;
+    int32_t material[RT_MAX_FACES];
+    double transform[16];
+    double plane_point[3];
+    double plane_normal[3];
+} rt_object;
+
+/* gml.RenderArgs (internal/gml/evaluator.go:14-28) with the scene already
+ * flattened. depth <= 0 => 3 and fov <= 0 => 90 are applied by the library
+ * exactly as raytracer.go:592-600 does. */
+typedef struct rt_scene {
+    int32_t width;
+    int32_t height;
+    int32_t depth;
+    int32_t num_lights;
+    double fov;          /* degrees */
+    double ambient[3];
+    double bg_start[3];  /* BgColorStart (zero when plain `render`) */
+    double bg_end[3];    /* BgColorEnd */
+    const rt_point_light *lights;
+    const rt_object *objects;
+    const rt_material *materials;
+    int32_t num_objects;
+    int32_t num_materials;
+} rt_scene;
+
+/* Work counters, identical in the CPU oracle and the GPU path.
+ *   primary_rays     top-level traceRay calls (4 per pixel, raytracer.go:639)
+ *   secondary_rays   recursive traceRay calls entered with depth > 0
+ *                    (raytracer.go:528,554; depth 0 returns at :488-491)
+ *   shadow_rays      inShadow calls: one per (shaded hit, light)
+ *                    (raytracer.go:383)
+ *   tests[k]         Intersect calls on kind k made by closestHit
+ *   shadow_tests[k]  Intersect calls on kind k made by inShadow (early exit)
+ *   shaded_hits      ComputeSurfaceProps + computeLighting evaluations */
+typedef struct rt_stats {
+    uint64_t primary_rays;
+    uint64_t secondary_rays;
+    uint64_t shadow_rays;
+    uint64_t tests[RT_NUM_KINDS];
+    uint64_t shadow_tests[RT_NUM_KINDS];
+    uint64_t shaded_hits;
+    double kernel_ms;    /* device time of the last render (GPU path)  */
+} rt_stats;
+
+/* Opaque per-device context: owns the converted scene on the device, the
+ * work-queue counters and the stats buffer. Re-usable across renders (the
+ * reference REPL renders many times per process, cmd/gml/main.go:104-115). */
+typedef struct rt_context rt_context;
+
+/* ABI version of the loaded library (RT_ABI_VERSION). */
+int rt_abi_version(void);
+
+/* Thread-local description of the last failure on this thread. */
+const char *rt_last_error(void);
+
+/* Create a context on HIP device `device` (the caller's current device when
+ * device < 0). */
+int rt_create(int device, rt_context **out);
+void rt_destroy(rt_context *ctx);
+
+/* Convert the flattened scene exactly as ConvertRenderArgsToScene
+ * (raytracer.go:724-830) and upload it to the context's device. The scene is
+ * read only during the call. Replaces any previous scene. */
+int rt_set_scene(rt_context *ctx, const rt_scene *scene);
+
+/* Enqueue the render of image rows [y0, y1) on `stream` (a hipStream_t; NULL
+ * = the null stream) into device memory `d_rgba` (row y0 first, stride
+ * 4*width bytes). Asynchronous; device pointers only. The per-row pixels are
+ * identical to rows y0..y1-1 of a full-frame Render(): RNG state depends only
+ * on (x, 20-row strip) (raytracer.go:627-634). */
+int rt_render_rows_async(rt_context *ctx, int y0, int y1, void *d_rgba,
+                         void *stream);
+
+/* Read (and optionally reset) the work counters accumulated on the device
+ * since the last reset. Synchronises the given stream. */
+int rt_read_stats(rt_context *ctx, void *stream, int reset, rt_stats *out);
+
+/* Device time (ms) of the most recent rt_render_rows_async on this context,
+ * measured with HIP events on the stream it was launched on. Synchronises. */
+int rt_last_kernel_ms(rt_context *ctx, double *ms_out);
+
+/* Convenience, synchronous whole-frame Render() into host memory
+ * (width*height*4 bytes, caller-owned). Uses a cached context on the
+ * current device. stats may be NULL. Includes PCIe transfers. */
+int rt_render(const rt_scene *scene, uint8_t *rgba_out, rt_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_ABI_H */

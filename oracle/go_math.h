@@ -1,0 +1,256 @@
+/*
+ * go_math.h -- TEST INFRASTRUCTURE (oracle). Plain-C restatement of the Go
+ * standard-library arithmetic the reference's render path calls. Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+ * anything under oracle/.
+ *
+ * Third-party source (absent from /root/reference): the Go standard library
+ * at the reference's `go 1.24.5` directive (go.mod:3). Restated here from the
+ * published algorithms:
+ *   math.Max / math.Min        (dim.go; amd64 assembly has the same semantics)
+ *   math.Pow                   (pow.go: Frexp + repeated squaring, Ldexp)
+ *   math.Tan / math.Sin / Cos  (tan.go, sin.go: Cephes, Cody-Waite reduction)
+ *   math/rand/v2 PCG + Float64 (pcg.go: 128-bit LCG, DXSM output;
+ *                               rand.go: Float64 = (u<<11>>11) / 2^53)
+ *   float64 -> uint32 conversion on amd64 (CVTTSD2SQ then truncate)
+ * Compiled with -ffp-contract=off: Go on amd64 (GOAMD64=v1) fuses no
+ * multiply-adds.
+ */
+#ifndef GO_MATH_H
+#define GO_MATH_H
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+static inline uint64_t go_f64bits(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
+static inline double go_f64frombits(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
+static inline int go_signbit(double x) { return (int)(go_f64bits(x) >> 63); }
+
+/* math.Max (dim.go): +Inf wins, then NaN, then max(+0,-0) = +0. */
+static inline double go_max(double x, double y) {
+    if (isinf(x) && x > 0) return x;
+    if (isinf(y) && y > 0) return y;
+    if (isnan(x) || isnan(y)) return NAN;
+    if (x == 0 && x == y) return go_signbit(x) ? y : x;
+    return x > y ? x : y;
+}
+
+/* math.Min (dim.go): -Inf wins, then NaN, then min(+0,-0) = -0. */
+static inline double go_min(double x, double y) {
+    if (isinf(x) && x < 0) return x;
+    if (isinf(y) && y < 0) return y;
+    if (isnan(x) || isnan(y)) return NAN;
+    if (x == 0 && x == y) return go_signbit(x) ? x : y;
+    return x < y ? x : y;
+}
+
+/* math.Frexp: frac in [0.5,1), normalises subnormals. */
+static inline double go_frexp(double f, int *e) {
+    *e = 0;
+    if (f == 0 || isinf(f) || isnan(f)) return f;
+    return frexp(f, e);
+}
+
+/* math.Modf for f >= 0 (Pow only calls it on Abs(y)). */
+static inline double go_modf(double f, double *frac) {
+    double ip;
+    if (f < 1) {
+        if (f < 0) { double fr; ip = -go_modf(-f, &fr); *frac = -fr; return ip; }
+        if (f == 0) { *frac = f; return f; }
+        *frac = f; return 0;
+    }
+    ip = trunc(f);
+    *frac = f - ip;
+    return ip;
+}
+
+static inline int go_is_odd_int(double x) {
+    if (fabs(x) >= (double)(1ULL << 53)) return 0;
+    double xf;
+    double xi = go_modf(x, &xf);
+    return xf == 0 && ((int64_t)xi & 1) == 1;
+}
+
+/* math.Ldexp: exact scaling with a single rounding for subnormal results --
+ * identical to C ldexp for every finite input. */
+static inline double go_ldexp(double frac, int e) { return ldexp(frac, e); }
+
+/* Fractional part of Pow needs Exp/Log. The reference scenes only use
+ * integer exponents (specular n, Schlick 5); for a fractional exponent we use
+ * libm exp/log, which is NOT guaranteed bit-identical to Go's amd64 assembly
+ * Exp/Log -- parity for fractional specular exponents is unpinned. */
+static inline double go_pow(double x, double y) {
+    if (y == 0 || x == 1) return 1;
+    if (y == 1) return x;
+    if (isnan(x) || isnan(y)) return NAN;
+    if (x == 0) {
+        if (y < 0) {
+            if (go_signbit(x) && go_is_odd_int(y)) return -INFINITY;
+            return INFINITY;
+        }
+        if (y > 0) {
+            if (go_signbit(x) && go_is_odd_int(y)) return x;
+            return 0;
+        }
+    }
+    if (isinf(y)) {
+        if (x == -1) return 1;
+        if ((fabs(x) < 1) == (y > 0)) return 0;
+        return INFINITY;
+    }
+    if (isinf(x)) {
+        if (x < 0) return go_pow(1 / x, -y);
+        if (y < 0) return 0;
+        if (y > 0) return INFINITY;
+    }
+    if (y == 0.5) return sqrt(x);
+    if (y == -0.5) return 1 / sqrt(x);
+
+    double yf;
+    double yi = go_modf(fabs(y), &yf);
+    if (yf != 0 && x < 0) return NAN;
+    if (yi >= 9223372036854775808.0) {
+        if (x == -1) return 1;
+        if ((fabs(x) < 1) == (y > 0)) return 0;
+        return INFINITY;
+    }
+    double a1 = 1.0;
+    int ae = 0;
+    if (yf != 0) {
+        if (yf > 0.5) { yf--; yi++; }
+        a1 = exp(yf * log(x));
+    }
+    int xe;
+    double x1 = go_frexp(x, &xe);
+    for (int64_t i = (int64_t)yi; i != 0; i >>= 1) {
+        if (xe < -(1 << 12) || (1 << 12) < xe) {
+            ae += xe;
+            break;
+        }
+        if ((i & 1) == 1) { a1 *= x1; ae += xe; }
+        x1 *= x1;
+        xe <<= 1;
+        if (x1 < .5) { x1 += x1; xe--; }
+    }
+    if (y < 0) { a1 = 1 / a1; ae = -ae; }
+    return go_ldexp(a1, ae);
+}
+
+/* Cephes coefficients as in Go's sin.go / tan.go. */
+static const double go_sin_c[6] = {
+    1.58962301576546568060e-10, -2.50507477628578072866e-8,
+    2.75573136213857245213e-6,  -1.98412698295895385996e-4,
+    8.33333333332211858878e-3,  -1.66666666666666307295e-1,
+};
+static const double go_cos_c[6] = {
+    -1.13585365213876817300e-11, 2.08757008419747316778e-9,
+    -2.75573141792967388112e-7,  2.48015872888517045348e-5,
+    -1.38888888888730564116e-3,  4.16666666666665929218e-2,
+};
+static const double go_tanP[3] = {
+    -1.30936939181383777646e4, 1.15351664838587416140e6, -1.79565251976484877988e7,
+};
+static const double go_tanQ[5] = {
+    1.0, 1.36812963470692954678e4, -1.32089234440210967447e6,
+    2.50083801823357915839e7, -5.38695755929454629881e7,
+};
+#define GO_PI4A 7.85398125648498535156e-1
+#define GO_PI4B 3.77489470793079817668e-8
+#define GO_PI4C 2.69515142907905952645e-15
+#define GO_4_OVER_PI 1.2732395447351628 /* const 4/Pi rounded once: 0x3ff45f306dc9c883 */
+#define GO_REDUCE_THRESHOLD ((double)(1 << 29))
+
+/* Arguments >= 2^29 need Payne-Hanek (trigReduce); the render path only uses
+ * fov/2 and fuzz values, far below it. Callers check. */
+static inline double go_sin(double x) {
+    if (x == 0 || isnan(x)) return x;
+    if (isinf(x)) return NAN;
+    int sign = 0;
+    if (x < 0) { x = -x; sign = 1; }
+    uint64_t j = (uint64_t)(x * GO_4_OVER_PI);
+    double y = (double)j;
+    if ((j & 1) == 1) { j++; y++; }
+    j &= 7;
+    double z = ((x - y * GO_PI4A) - y * GO_PI4B) - y * GO_PI4C;
+    if (j > 3) { sign = !sign; j -= 4; }
+    double zz = z * z;
+    if (j == 1 || j == 2)
+        y = 1.0 - 0.5 * zz + zz * zz * ((((((go_cos_c[0] * zz) + go_cos_c[1]) * zz + go_cos_c[2]) * zz + go_cos_c[3]) * zz + go_cos_c[4]) * zz + go_cos_c[5]);
+    else
+        y = z + z * zz * ((((((go_sin_c[0] * zz) + go_sin_c[1]) * zz + go_sin_c[2]) * zz + go_sin_c[3]) * zz + go_sin_c[4]) * zz + go_sin_c[5]);
+    return sign ? -y : y;
+}
+
+static inline double go_cos(double x) {
+    if (isnan(x) || isinf(x)) return NAN;
+    int sign = 0;
+    x = fabs(x);
+    uint64_t j = (uint64_t)(x * GO_4_OVER_PI);
+    double y = (double)j;
+    if ((j & 1) == 1) { j++; y++; }
+    j &= 7;
+    double z = ((x - y * GO_PI4A) - y * GO_PI4B) - y * GO_PI4C;
+    if (j > 3) { j -= 4; sign = !sign; }
+    if (j > 1) sign = !sign;
+    double zz = z * z;
+    if (j == 1 || j == 2)
+        y = z + z * zz * ((((((go_sin_c[0] * zz) + go_sin_c[1]) * zz + go_sin_c[2]) * zz + go_sin_c[3]) * zz + go_sin_c[4]) * zz + go_sin_c[5]);
+    else
+        y = 1.0 - 0.5 * zz + zz * zz * ((((((go_cos_c[0] * zz) + go_cos_c[1]) * zz + go_cos_c[2]) * zz + go_cos_c[3]) * zz + go_cos_c[4]) * zz + go_cos_c[5]);
+    return sign ? -y : y;
+}
+
+static inline double go_tan(double x) {
+    if (x == 0 || isnan(x)) return x;
+    if (isinf(x)) return NAN;
+    int sign = 0;
+    if (x < 0) { x = -x; sign = 1; }
+    uint64_t j = (uint64_t)(x * GO_4_OVER_PI);
+    double y = (double)j;
+    if ((j & 1) == 1) { j++; y++; }
+    double z = ((x - y * GO_PI4A) - y * GO_PI4B) - y * GO_PI4C;
+    double zz = z * z;
+    if (zz > 1e-14)
+        y = z + z * (zz * (((go_tanP[0] * zz) + go_tanP[1]) * zz + go_tanP[2]) /
+                     ((((zz + go_tanQ[1]) * zz + go_tanQ[2]) * zz + go_tanQ[3]) * zz + go_tanQ[4]));
+    else
+        y = z;
+    if ((j & 2) == 2) y = -1 / y;
+    return sign ? -y : y;
+}
+
+/* math/rand/v2 PCG (pcg.go): state = state*mul + inc mod 2^128; DXSM. */
+typedef struct go_pcg { uint64_t hi, lo; } go_pcg;
+
+static inline uint64_t go_pcg_uint64(go_pcg *p) {
+    const uint64_t mulHi = 2549297995355413924ULL, mulLo = 4865540595714422341ULL;
+    const uint64_t incHi = 6364136223846793005ULL, incLo = 1442695040888963407ULL;
+    unsigned __int128 m = (unsigned __int128)p->lo * mulLo;
+    uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
+    hi += p->hi * mulLo + p->lo * mulHi;
+    uint64_t lo2 = lo + incLo;
+    uint64_t c = lo2 < lo;
+    hi = hi + incHi + c;
+    p->lo = lo2;
+    p->hi = hi;
+    hi ^= hi >> 32;
+    hi *= 0xda942042e4dd58b5ULL;
+    hi ^= hi >> 48;
+    hi *= (lo2 | 1);
+    return hi;
+}
+
+/* rand.go: Float64 = float64(Uint64()<<11>>11) / (1<<53). */
+static inline double go_rand_float64(go_pcg *p) {
+    return (double)(go_pcg_uint64(p) << 11 >> 11) / 9007199254740992.0;
+}
+
+/* uint32(v) for float64 v on amd64: CVTTSD2SQ (int64, "indefinite"
+ * 0x8000000000000000 on NaN/overflow), then the low 32 bits. */
+static inline uint32_t go_f64_to_u32(double v) {
+    if (!(v > -9223372036854775808.0 && v < 9223372036854775808.0)) return 0u;
+    return (uint32_t)(uint64_t)(int64_t)v;
+}
+
+#endif /* GO_MATH_H */

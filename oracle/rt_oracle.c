@@ -1,0 +1,593 @@
+/*
+ * rt_oracle.c -- TEST INFRASTRUCTURE, not product code.
+ *
+ * A plain-C, FP64, single-rounding-per-op restatement of the reference's
+ * render hot path (timdestan/go-raytracer), used only as the parity checker
+ * by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg. The
+ * product path (go-raytracer_amd/) never links, loads or calls this file.
+ *
+ * Parity pin: tests/test_oracle.py renders internal/gml/testdata/canned.gml's
+ * scene and compares byte-for-byte with the reference's own golden
+ * testdata/goldens/example_canned.png (committed as tests/golden/), plus the
+ * Cylinder known-answer tests of cylinder_test.go:21-165.
+ *
+ * Every function cites the reference line it follows. Build:
+ * oracle/Makefile (-O2 -ffp-contract=off; Go on amd64 fuses no FMAs).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/rt_abi.h"
+#include "go_math.h"
+
+/* ---- prim.Vec3 (internal/prim/vec.go:9-121) ---------------------------- */
+typedef struct { double x, y, z; } vec3;
+
+static inline vec3 V(double x, double y, double z) { vec3 r = {x, y, z}; return r; }
+static inline vec3 v_add(vec3 a, vec3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }        /* :23 */
+static inline vec3 v_sub(vec3 a, vec3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }        /* :31 */
+static inline vec3 v_mul(vec3 a, vec3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }        /* :40 */
+static inline double v_dot(vec3 a, vec3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }        /* :48 */
+static inline vec3 v_scale(vec3 a, double s) { return V(a.x * s, a.y * s, a.z * s); }          /* :70 */
+static inline double v_len(vec3 v) { return sqrt(v.x * v.x + v.y * v.y + v.z * v.z); }         /* :95 */
+static inline vec3 v_norm(vec3 v) {                                                             /* :78 */
+    double m = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+    return V(v.x / m, v.y / m, v.z / m);
+}
+static inline vec3 v_neg(vec3 v) { return V(-v.x, -v.y, -v.z); }                               /* :87 */
+static inline vec3 v_lerp(vec3 a, vec3 b, double t) {                                           /* :56 */
+    return V(a.x + (b.x - a.x) * t, a.y + (b.y - a.y) * t, a.z + (b.z - a.z) * t);
+}
+static inline int v_iszero(vec3 v) { return v.x == 0.0 && v.y == 0.0 && v.z == 0.0; }          /* :99 */
+static inline double clampd(double lo, double hi, double x) { return go_min(go_max(x, lo), hi); } /* :218 */
+static inline vec3 v_clamp(vec3 c) { return V(clampd(0, 1, c.x), clampd(0, 1, c.y), clampd(0, 1, c.z)); } /* :110 */
+static inline double v_cos_sim(vec3 a, vec3 b) { return v_dot(a, b) / (v_len(a) * v_len(b)); }  /* :52 */
+
+/* ---- prim.Mat4 (vec.go:256-425) ----------------------------------------- */
+typedef struct { double m[4][4]; } mat4;
+
+static mat4 m_identity(void) {
+    mat4 r; memset(&r, 0, sizeof r);
+    r.m[0][0] = r.m[1][1] = r.m[2][2] = r.m[3][3] = 1.0;
+    return r;
+}
+static mat4 m_transpose(const mat4 *a) {                                                       /* :288 */
+    mat4 r;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) r.m[i][j] = a->m[j][i];
+    return r;
+}
+static inline vec3 m_mulpoint(const mat4 *a, vec3 v) {                                         /* :298 */
+    return V(a->m[0][0] * v.x + a->m[0][1] * v.y + a->m[0][2] * v.z + a->m[0][3],
+             a->m[1][0] * v.x + a->m[1][1] * v.y + a->m[1][2] * v.z + a->m[1][3],
+             a->m[2][0] * v.x + a->m[2][1] * v.y + a->m[2][2] * v.z + a->m[2][3]);
+}
+static inline vec3 m_muldir(const mat4 *a, vec3 v) {                                           /* :307 */
+    return V(a->m[0][0] * v.x + a->m[0][1] * v.y + a->m[0][2] * v.z,
+             a->m[1][0] * v.x + a->m[1][1] * v.y + a->m[1][2] * v.z,
+             a->m[2][0] * v.x + a->m[2][1] * v.y + a->m[2][2] * v.z);
+}
+/* Affine inverse, vec.go:319-365. Returns 0 when det == 0 (Go returns nil). */
+static int m_inverse(const mat4 *M, mat4 *out) {
+    const double(*m)[4] = M->m;
+    double a = m[0][0], b = m[0][1], c = m[0][2];
+    double d = m[1][0], e = m[1][1], f = m[1][2];
+    double g = m[2][0], h = m[2][1], i = m[2][2];
+    double det = a * (e * i - f * h) - b * (d * i - f * g) + c * (d * h - e * g);
+    if (det == 0.0) return 0;
+    mat4 inv;
+    inv.m[0][0] = (e * i - f * h) / det; inv.m[0][1] = (c * h - b * i) / det; inv.m[0][2] = (b * f - c * e) / det; inv.m[0][3] = 0.0;
+    inv.m[1][0] = (f * g - d * i) / det; inv.m[1][1] = (a * i - c * g) / det; inv.m[1][2] = (c * d - a * f) / det; inv.m[1][3] = 0.0;
+    inv.m[2][0] = (d * h - e * g) / det; inv.m[2][1] = (b * g - a * h) / det; inv.m[2][2] = (a * e - b * d) / det; inv.m[2][3] = 0.0;
+    inv.m[3][0] = 0.0; inv.m[3][1] = 0.0; inv.m[3][2] = 0.0; inv.m[3][3] = 1.0;
+    inv.m[0][3] = -(inv.m[0][0] * m[0][3] + inv.m[0][1] * m[1][3] + inv.m[0][2] * m[2][3]);
+    inv.m[1][3] = -(inv.m[1][0] * m[0][3] + inv.m[1][1] * m[1][3] + inv.m[1][2] * m[2][3]);
+    inv.m[2][3] = -(inv.m[2][0] * m[0][3] + inv.m[2][1] * m[1][3] + inv.m[2][2] * m[2][3]);
+    *out = inv;
+    return 1;
+}
+
+/* ---- converted scene objects (raytracer.go:43-277, 756-830) ------------- */
+typedef struct {
+    int side;              /* prim.CubeSide, 0 if not part of a cube */
+    vec3 normal;           /* object-space normal */
+    double d;              /* -normal.Dot(point), raytracer.go:768 */
+    vec3 normal_world;     /* W2O^T * normal, normalised, raytracer.go:767 */
+} plane_face;
+
+typedef struct {
+    int kind;
+    int material[RT_MAX_FACES];
+    mat4 o2w, w2o, normal_mat;
+    plane_face face[RT_MAX_FACES]; /* plane: face[0]; cube: 6 faces */
+} object;
+
+typedef struct {
+    int width, height, depth;
+    double vw, vh;
+    vec3 ambient, bg0, bg1;
+    int nlights;
+    vec3 *lpos, *lcol;
+    int nobj;
+    object *obj;
+    const rt_material *mats;
+    int nmats;
+} scene;
+
+typedef struct { vec3 origin, dir; } ray;
+typedef struct { int obj; double t; vec3 p; int face; } hit; /* raytracer.go:21-28 */
+
+/* prim.PlanesForUnitCube, internal/prim/plane.go:29-38 */
+static const double cube_pts[6][3] = {{0, 0, 0}, {0, 0, 1}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 0}};
+static const double cube_nrm[6][3] = {{0, 0, -1}, {0, 0, 1}, {-1, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, -1, 0}};
+
+static plane_face create_plane(vec3 point, vec3 normal, const mat4 *w2o) {      /* raytracer.go:764-774 */
+    plane_face p;
+    p.side = 0;
+    p.normal = normal;
+    mat4 t = m_transpose(w2o);
+    p.normal_world = v_norm(m_muldir(&t, normal));
+    p.d = -v_dot(normal, point);
+    return p;
+}
+
+/* ---- Intersect (raytracer.go:51-337) ------------------------------------ */
+static inline ray to_object(ray r, const mat4 *w2o) {                            /* :51-56 */
+    ray l;
+    l.origin = m_mulpoint(w2o, r.origin);
+    l.dir = m_muldir(w2o, r.dir);
+    return l;
+}
+
+static int sphere_intersect(const object *o, ray r, double *t, vec3 *p) {       /* :58-104 */
+    r = to_object(r, &o->w2o);
+    vec3 oc = r.origin;
+    double a = v_dot(r.dir, r.dir);
+    double halfB = v_dot(oc, r.dir);
+    double c = v_dot(oc, oc) - 1.0;
+    double disc = halfB * halfB - a * c;
+    if (disc < 0.0) return 0;
+    double sq = sqrt(disc);
+    double t0 = (-halfB - sq) / a;
+    if (t0 > 0.0) {
+        *t = t0;
+        *p = v_add(r.origin, v_scale(r.dir, t0));
+        return 1;
+    }
+    return 0;
+}
+
+static int plane_intersect_obj(const plane_face *f, ray lr, double *t, vec3 *p) { /* :164-180 (ray already in object space) */
+    double denom = v_dot(f->normal, lr.dir);
+    if (fabs(denom) < 1e-6) return 0;
+    double tt = (-f->d - v_dot(f->normal, lr.origin)) / denom;
+    if (tt <= 0.0) return 0;
+    *t = tt;
+    *p = v_add(lr.origin, v_scale(lr.dir, tt));
+    return 1;
+}
+
+static int cube_intersect(const object *o, ray r, double *t, vec3 *p, int *face) { /* :214-240 */
+    int found = 0;
+    double best = 0;
+    vec3 bp = V(0, 0, 0);
+    int bf = 0;
+    for (int fi = 0; fi < 6; fi++) {
+        /* Each face re-transforms the ray with the same matrix (:165): same result. */
+        ray lr = to_object(r, &o->w2o);
+        double ft; vec3 fp;
+        if (!plane_intersect_obj(&o->face[fi], lr, &ft, &fp)) continue;
+        if (ft < 0.0) continue;
+        if (fp.x < 0 || fp.x > 1 || fp.y < 0 || fp.y > 1 || fp.z < 0 || fp.z > 1) continue;
+        if (!found || ft < best) { found = 1; best = ft; bp = fp; bf = fi; }
+    }
+    if (found) { *t = best; *p = bp; *face = bf; }
+    return found;
+}
+
+static int cylinder_intersect(const object *o, ray r, double *t, vec3 *p, int *face) { /* :279-337 */
+    r = to_object(r, &o->w2o);
+    double bestT = INFINITY;
+    int bestFace = -1;
+    vec3 bestP = V(0, 0, 0);
+#define CONSIDER(tt, ff, pp) do { if ((tt) > 0.0 && (tt) < bestT) { bestT = (tt); bestFace = (ff); bestP = (pp); } } while (0)
+    double a = r.dir.x * r.dir.x + r.dir.z * r.dir.z;
+    if (a > 1e-12) {
+        double halfB = r.origin.x * r.dir.x + r.origin.z * r.dir.z;
+        double c0 = r.origin.x * r.origin.x + r.origin.z * r.origin.z - 1.0;
+        double disc = halfB * halfB - a * c0;
+        if (disc >= 0.0) {
+            double sq = sqrt(disc);
+            double ts[2] = {(-halfB - sq) / a, (-halfB + sq) / a};
+            for (int k = 0; k < 2; k++) {
+                vec3 pt = v_add(r.origin, v_scale(r.dir, ts[k]));
+                if (pt.y >= 0.0 && pt.y <= 1.0) CONSIDER(ts[k], 0, pt);
+            }
+        }
+    }
+    if (fabs(r.dir.y) > 1e-12) {
+        double tTop = (1.0 - r.origin.y) / r.dir.y;
+        vec3 pTop = v_add(r.origin, v_scale(r.dir, tTop));
+        if (pTop.x * pTop.x + pTop.z * pTop.z <= 1.0) CONSIDER(tTop, 1, pTop);
+        double tBot = -r.origin.y / r.dir.y;
+        vec3 pBot = v_add(r.origin, v_scale(r.dir, tBot));
+        if (pBot.x * pBot.x + pBot.z * pBot.z <= 1.0) CONSIDER(tBot, 2, pBot);
+    }
+#undef CONSIDER
+    if (bestFace == -1) return 0;
+    *t = bestT; *p = bestP; *face = bestFace;
+    return 1;
+}
+
+static int object_intersect(const object *o, ray r, double *t, vec3 *p, int *face) {
+    *face = 0;
+    switch (o->kind) {
+    case RT_SPHERE: return sphere_intersect(o, r, t, p);
+    case RT_PLANE: { ray lr = to_object(r, &o->w2o); return plane_intersect_obj(&o->face[0], lr, t, p); }
+    case RT_CUBE: return cube_intersect(o, r, t, p, face);
+    case RT_CYLINDER: return cylinder_intersect(o, r, t, p, face);
+    }
+    return 0;
+}
+
+/* ---- per-thread counters ------------------------------------------------ */
+typedef struct { uint64_t secondary, shadow, tests[4], shadow_tests[4], shaded; } counters;
+
+static int closest_hit(const scene *s, ray r, hit *h, counters *cnt) {          /* :469-483 */
+    int found = 0;
+    for (int i = 0; i < s->nobj; i++) {
+        double t; vec3 p; int f;
+        cnt->tests[s->obj[i].kind]++;
+        if (!object_intersect(&s->obj[i], r, &t, &p, &f)) continue;
+        if (!found || t < h->t) { found = 1; h->obj = i; h->t = t; h->p = p; h->face = f; }
+    }
+    return found;
+}
+
+typedef struct { vec3 pw, nw; const rt_material *mat; } hitex;                  /* :31-36 */
+
+static void surface_props(const scene *s, const hit *h, hitex *x) {
+    const object *o = &s->obj[h->obj];
+    switch (o->kind) {
+    case RT_SPHERE:                                                             /* :106-122 */
+        x->pw = m_mulpoint(&o->o2w, h->p);
+        x->nw = h->p;
+        break;
+    case RT_PLANE:                                                              /* :182-194 */
+        x->pw = m_mulpoint(&o->o2w, h->p);
+        x->nw = o->face[0].normal_world;
+        break;
+    case RT_CUBE:                                                               /* :242-260 */
+        x->pw = m_mulpoint(&o->o2w, h->p);
+        x->nw = o->face[h->face].normal_world;
+        break;
+    case RT_CYLINDER: {                                                         /* :339-370 */
+        vec3 n;
+        if (h->face == 0) n = V(h->p.x, 0, h->p.z);
+        else if (h->face == 1) n = V(0, 1, 0);
+        else n = V(0, -1, 0);
+        x->pw = m_mulpoint(&o->o2w, h->p);
+        x->nw = v_norm(m_muldir(&o->normal_mat, n));
+        break;
+    }
+    }
+    x->mat = &s->mats[o->material[h->face]];
+}
+
+static int in_shadow(const scene *s, const hit *h, const hitex *x, vec3 ldir, double dist, ray r, counters *cnt) { /* :411-429 */
+    const double eps = 1e-4;
+    ray sr;
+    sr.origin = v_add(x->pw, v_scale(x->nw, eps));
+    sr.dir = ldir;
+    for (int i = 0; i < s->nobj; i++) {
+        if (i == h->obj) continue;
+        double t; vec3 p; int f;
+        cnt->shadow_tests[s->obj[i].kind]++;
+        if (!object_intersect(&s->obj[i], sr, &t, &p, &f)) continue;
+        if (t * v_len(r.dir) < dist) return 1;
+    }
+    return 0;
+}
+
+static vec3 compute_lighting(const scene *s, const hit *h, const hitex *x, ray r, counters *cnt) { /* :372-401 */
+    vec3 Vv = v_neg(r.dir);
+    const rt_material *mat = x->mat;
+    vec3 result = v_scale(s->ambient, mat->kd);
+    for (int li = 0; li < s->nlights; li++) {
+        vec3 lth = v_sub(s->lpos[li], x->pw);
+        double dist = v_len(lth);
+        vec3 ldir = v_norm(lth);
+        cnt->shadow++;
+        if (in_shadow(s, h, x, ldir, dist, r, cnt)) continue;
+        double ndl = go_max(0, v_dot(x->nw, ldir));
+        vec3 diffuse = v_scale(s->lcol[li], ndl * mat->kd);
+        vec3 H = v_norm(v_add(Vv, ldir));
+        double spec = go_max(0, v_dot(x->nw, H));
+        vec3 specular = v_scale(s->lcol[li], mat->ks * go_pow(spec, mat->specular_exponent));
+        result = v_add(v_add(result, diffuse), specular);
+    }
+    return result;
+}
+
+static vec3 refract(vec3 inc, vec3 n, double n1, double n2) {                   /* :438-450 */
+    double ratio = n1 / n2;
+    double cosI = -v_dot(n, inc);
+    double sinT2 = ratio * ratio * (1.0 - cosI * cosI);
+    if (sinT2 > 1.0) return V(0, 0, 0);
+    double cosT = sqrt(1.0 - sinT2);
+    return v_add(v_scale(inc, ratio), v_scale(n, ratio * cosI - cosT));
+}
+
+static double fresnel(vec3 n, vec3 inc, double ior) {                           /* :456-467 */
+    double cosi = v_cos_sim(inc, n);
+    double etai = 1.0, etat = ior;
+    double r0 = (etai - etat) / (etai + etat);
+    r0 = r0 * r0;
+    double cost = fabs(cosi);
+    return r0 + (1 - r0) * go_pow(1 - cost, 5);
+}
+
+static vec3 trace_ray(const scene *s, ray r, int depth, counters *cnt) {        /* :487-562 */
+    if (depth <= 0) return V(0, 0, 0);
+    hit h;
+    if (!closest_hit(s, r, &h, cnt)) {
+        double t = 0.5 * (r.dir.y + 1.0);
+        return v_lerp(s->bg0, s->bg1, t);
+    }
+    hitex x;
+    surface_props(s, &h, &x);
+    cnt->shaded++;
+    vec3 lighting = compute_lighting(s, &h, &x, r, cnt);
+    const rt_material *mat = x.mat;
+    vec3 col = V(mat->color[0], mat->color[1], mat->color[2]);
+    if (mat->reflectivity == 0 && mat->transparency == 0) return v_clamp(v_mul(lighting, col));
+
+    vec3 reflected = V(0, 0, 0);
+    if (mat->reflectivity > 0) {
+        vec3 rd = v_sub(r.dir, v_scale(x.nw, 2.0 * v_dot(r.dir, x.nw)));
+        double fuzz = mat->fuzziness;
+        if (fuzz >= 0) {
+            double cf = go_cos(fuzz), sf = go_sin(fuzz);
+            rd = v_add(rd, V(fuzz * cf * cf, fuzz * sf * sf, 0));
+        }
+        ray rr;
+        rr.origin = v_add(x.pw, v_scale(x.nw, 1e-4));
+        rr.dir = v_norm(rd);
+        if (depth - 1 > 0) cnt->secondary++;
+        reflected = trace_ray(s, rr, depth - 1, cnt);
+    }
+    vec3 refracted = V(0, 0, 0);
+    if (mat->transparency > 0) {
+        double n1 = 1.0, n2 = mat->refractive_index;
+        vec3 normal = x.nw;
+        if (v_dot(r.dir, normal) > 0.0) {
+            double tmp = n1; n1 = n2; n2 = tmp;
+            normal = v_scale(normal, -1.0);
+        }
+        vec3 rd = refract(r.dir, normal, n1, n2);
+        if (!v_iszero(rd)) {
+            ray tr;
+            tr.origin = v_sub(x.pw, v_scale(normal, 1e-4));
+            tr.dir = rd;
+            if (depth - 1 > 0) cnt->secondary++;
+            refracted = trace_ray(s, tr, depth - 1, cnt);
+        }
+    }
+    if (mat->transparency == 0)
+        return v_clamp(v_mul(v_add(lighting, v_scale(reflected, mat->reflectivity)), col));
+    double kr = fresnel(x.nw, r.dir, mat->refractive_index);
+    return v_clamp(v_mul(v_add(v_scale(lighting, 1.0 - mat->transparency),
+                               v_add(v_scale(reflected, kr), v_scale(refracted, 1.0 - kr))),
+                         col));
+}
+
+/* ---- scene conversion (raytracer.go:592-603, 724-830) -------------------- */
+static int convert_scene(const rt_scene *in, scene *s) {
+    memset(s, 0, sizeof *s);
+    if (in->width <= 0 || in->height <= 0 || in->num_objects < 0 || in->num_lights < 0) return RT_E_INVALID;
+    s->width = in->width;
+    s->height = in->height;
+    s->depth = in->depth <= 0 ? 3 : in->depth;                                  /* :592-595 */
+    double fov = in->fov <= 0.0 ? 90.0 : in->fov;                               /* :597-600 */
+    double fovr = fov * M_PI / 180.0;                                           /* :601 */
+    s->vw = 2.0 / go_tan(fovr / 2.0);                                           /* :602 */
+    s->vh = s->vw * ((double)in->height / (double)in->width);                   /* :603 */
+    s->ambient = V(in->ambient[0], in->ambient[1], in->ambient[2]);
+    s->bg0 = V(in->bg_start[0], in->bg_start[1], in->bg_start[2]);
+    s->bg1 = V(in->bg_end[0], in->bg_end[1], in->bg_end[2]);
+    s->nlights = in->num_lights;
+    s->lpos = (vec3 *)calloc((size_t)(in->num_lights + 1), sizeof(vec3));
+    s->lcol = (vec3 *)calloc((size_t)(in->num_lights + 1), sizeof(vec3));
+    for (int i = 0; i < in->num_lights; i++) {
+        s->lpos[i] = V(in->lights[i].position[0], in->lights[i].position[1], in->lights[i].position[2]);
+        s->lcol[i] = V(in->lights[i].color[0], in->lights[i].color[1], in->lights[i].color[2]);
+    }
+    s->mats = in->materials;
+    s->nmats = in->num_materials;
+    s->nobj = in->num_objects;
+    s->obj = (object *)calloc((size_t)(in->num_objects + 1), sizeof(object));
+    for (int i = 0; i < in->num_objects; i++) {
+        const rt_object *src = &in->objects[i];
+        object *o = &s->obj[i];
+        o->kind = src->kind;
+        if (src->kind < 0 || src->kind >= RT_NUM_KINDS) return RT_E_INVALID;
+        for (int f = 0; f < RT_MAX_FACES; f++) {
+            o->material[f] = src->material[f];
+            if (src->material[f] < 0 || src->material[f] >= in->num_materials) return RT_E_INVALID;
+        }
+        if (src->has_transform) {                                               /* :757-762 */
+            memcpy(o->o2w.m, src->transform, sizeof(double) * 16);
+            if (!m_inverse(&o->o2w, &o->w2o)) return RT_E_SINGULAR;
+        } else {
+            o->o2w = m_identity();
+            o->w2o = m_identity();
+        }
+        o->normal_mat = m_transpose(&o->w2o);                                   /* :790, :814 */
+        if (o->kind == RT_PLANE) {
+            o->face[0] = create_plane(V(src->plane_point[0], src->plane_point[1], src->plane_point[2]),
+                                      V(src->plane_normal[0], src->plane_normal[1], src->plane_normal[2]), &o->w2o);
+        } else if (o->kind == RT_CUBE) {                                        /* :799-803 */
+            for (int f = 0; f < 6; f++) {
+                o->face[f] = create_plane(V(cube_pts[f][0], cube_pts[f][1], cube_pts[f][2]),
+                                          V(cube_nrm[f][0], cube_nrm[f][1], cube_nrm[f][2]), &o->w2o);
+                o->face[f].side = f;
+            }
+        }
+    }
+    return RT_OK;
+}
+
+static void free_scene(scene *s) {
+    free(s->lpos); free(s->lcol); free(s->obj);
+}
+
+/* ---- Render (raytracer.go:589-682) --------------------------------------- */
+typedef struct {
+    const scene *s;
+    uint8_t *rgba;
+    int y0, y1;
+    int nstrips_y;
+    atomic_long next;
+    long total;
+    pthread_mutex_t lock;
+    counters sum;
+} job;
+
+static void render_strip(const scene *s, int x, int ymin, int y0, int y1, uint8_t *rgba, counters *cnt) {
+    go_pcg rng = {0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};          /* :632-634 */
+    int ymax = ymin + 20 < s->height ? ymin + 20 : s->height;                  /* :663-667 */
+    const vec3 eye = V(0.0, 0.0, -1.0);                                         /* :605-609 */
+    for (int y = ymin; y < ymax && y < y1; y++) {
+        vec3 total = V(0, 0, 0);
+        for (int k = 0; k < 4; k++) {                                           /* :639-652 */
+            double dx = go_rand_float64(&rng) - 0.5;
+            double dy = go_rand_float64(&rng) - 0.5;
+            if (y < y0) continue; /* rows before the band: draws consumed only */
+            double u = ((double)x + dx) / (double)(s->width - 1) * s->vw - s->vw / 2.0;
+            double v = ((double)y + dy) / (double)(s->height - 1) * s->vh - s->vh / 2.0;
+            ray r;
+            r.origin = V(u, -v, 0.0);
+            r.dir = v_norm(v_sub(r.origin, eye));
+            total = v_add(total, trace_ray(s, r, s->depth, cnt));
+        }
+        if (y < y0) continue;
+        vec3 c = v_scale(total, 1.0 / 4.0);                                     /* :656 */
+        uint8_t *px = rgba + ((size_t)(y - y0) * (size_t)s->width + (size_t)x) * 4;
+        px[0] = (uint8_t)(go_f64_to_u32(c.x * 65535.0) >> 8);                   /* vec.go:104-107 */
+        px[1] = (uint8_t)(go_f64_to_u32(c.y * 65535.0) >> 8);
+        px[2] = (uint8_t)(go_f64_to_u32(c.z * 65535.0) >> 8);
+        px[3] = 255;
+    }
+}
+
+static void *worker(void *arg) {
+    job *j = (job *)arg;
+    counters cnt;
+    memset(&cnt, 0, sizeof cnt);
+    const scene *s = j->s;
+    int sy0 = j->y0 / 20;
+    for (;;) {
+        long item = atomic_fetch_add(&j->next, 1);
+        if (item >= j->total) break;
+        int x = (int)(item / j->nstrips_y);
+        int ymin = (sy0 + (int)(item % j->nstrips_y)) * 20;
+        render_strip(s, x, ymin, j->y0, j->y1, j->rgba, &cnt);
+    }
+    pthread_mutex_lock(&j->lock);
+    j->sum.secondary += cnt.secondary;
+    j->sum.shadow += cnt.shadow;
+    j->sum.shaded += cnt.shaded;
+    for (int k = 0; k < 4; k++) { j->sum.tests[k] += cnt.tests[k]; j->sum.shadow_tests[k] += cnt.shadow_tests[k]; }
+    pthread_mutex_unlock(&j->lock);
+    return NULL;
+}
+
+/* Render rows [y0, y1) of the frame into rgba (row y0 first, stride 4W),
+ * using `threads` workers pulling (column, 20-row strip) items the way
+ * raytracer.go:611-679 does. */
+int oracle_render_rows(const rt_scene *in, int y0, int y1, int threads, uint8_t *rgba, rt_stats *st) {
+    scene s;
+    int rc = convert_scene(in, &s);
+    if (rc != RT_OK) { free_scene(&s); return rc; }
+    if (y0 < 0) y0 = 0;
+    if (y1 > s.height) y1 = s.height;
+    if (y1 <= y0) { free_scene(&s); return RT_E_INVALID; }
+    if (threads <= 0) threads = 8;                                              /* :725 */
+    job j;
+    memset(&j, 0, sizeof j);
+    j.s = &s;
+    j.rgba = rgba;
+    j.y0 = y0;
+    j.y1 = y1;
+    j.nstrips_y = (y1 - 1) / 20 - y0 / 20 + 1;
+    j.total = (long)s.width * j.nstrips_y;
+    atomic_init(&j.next, 0);
+    pthread_mutex_init(&j.lock, NULL);
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, worker, &j);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+    free(th);
+    pthread_mutex_destroy(&j.lock);
+    if (st) {
+        memset(st, 0, sizeof *st);
+        st->primary_rays = (uint64_t)4 * (uint64_t)s.width * (uint64_t)(y1 - y0);
+        st->secondary_rays = j.sum.secondary;
+        st->shadow_rays = j.sum.shadow;
+        st->shaded_hits = j.sum.shaded;
+        for (int k = 0; k < 4; k++) { st->tests[k] = j.sum.tests[k]; st->shadow_tests[k] = j.sum.shadow_tests[k]; }
+    }
+    free_scene(&s);
+    return RT_OK;
+}
+
+int oracle_render(const rt_scene *in, int threads, uint8_t *rgba, rt_stats *st) {
+    return oracle_render_rows(in, 0, in->height, threads, rgba, st);
+}
+
+/* ---- unit hooks for known-answer tests (cylinder_test.go) ---------------- */
+/* Intersect one converted object (object index `idx` of `in`) with a ray.
+ * Returns 1 on hit and fills t, point_obj[3], face. */
+int oracle_intersect(const rt_scene *in, int idx, const double origin[3], const double dir[3],
+                     double *t, double point_obj[3], int *face) {
+    scene s;
+    int rc = convert_scene(in, &s);
+    if (rc != RT_OK || idx < 0 || idx >= s.nobj) { free_scene(&s); return rc != RT_OK ? rc : RT_E_INVALID; }
+    ray r = {V(origin[0], origin[1], origin[2]), V(dir[0], dir[1], dir[2])};
+    vec3 p = V(0, 0, 0);
+    int f = 0;
+    double tt = 0;
+    int ok = object_intersect(&s.obj[idx], r, &tt, &p, &f);
+    if (ok) { *t = tt; point_obj[0] = p.x; point_obj[1] = p.y; point_obj[2] = p.z; *face = f; }
+    free_scene(&s);
+    return ok;
+}
+
+/* Surface normal for a given hit (ComputeSurfaceProps.NormalWorld). */
+int oracle_surface_normal(const rt_scene *in, int idx, int face, const double point_obj[3], double nw[3], double pw[3]) {
+    scene s;
+    int rc = convert_scene(in, &s);
+    if (rc != RT_OK || idx < 0 || idx >= s.nobj) { free_scene(&s); return rc != RT_OK ? rc : RT_E_INVALID; }
+    if (s.obj[idx].kind == RT_CYLINDER && (face < 0 || face > 2)) { free_scene(&s); return RT_E_INVALID; } /* :355-356 */
+    if (s.obj[idx].kind == RT_CUBE && (face < 0 || face >= 6)) { free_scene(&s); return RT_E_INVALID; }    /* :243-245 */
+    hit h = {idx, 0, V(point_obj[0], point_obj[1], point_obj[2]), face};
+    hitex x;
+    surface_props(&s, &h, &x);
+    nw[0] = x.nw.x; nw[1] = x.nw.y; nw[2] = x.nw.z;
+    pw[0] = x.pw.x; pw[1] = x.pw.y; pw[2] = x.pw.z;
+    free_scene(&s);
+    return RT_OK;
+}
+
+/* Go math restatements exposed for tests. */
+double oracle_go_pow(double x, double y) { return go_pow(x, y); }
+double oracle_go_tan(double x) { return go_tan(x); }
+double oracle_go_sin(double x) { return go_sin(x); }
+double oracle_go_cos(double x) { return go_cos(x); }
+void oracle_pcg_float64(uint64_t seed1, uint64_t seed2, int n, double *out) {
+    go_pcg p = {seed1, seed2};
+    for (int i = 0; i < n; i++) out[i] = go_rand_float64(&p);
+}

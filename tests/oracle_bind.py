@@ -1,0 +1,60 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) -- test infrastructure.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+
+_lib = None
+
+
+def build_oracle():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build_oracle()
+        l = C.CDLL(ORACLE_SO)
+        l.oracle_render_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        l.oracle_render_rows.restype = C.c_int
+        l.oracle_intersect.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]
+        l.oracle_intersect.restype = C.c_int
+        l.oracle_surface_normal.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                            C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        l.oracle_surface_normal.restype = C.c_int
+        for fn in ("oracle_go_pow",):
+            getattr(l, fn).argtypes = [C.c_double, C.c_double]
+            getattr(l, fn).restype = C.c_double
+        for fn in ("oracle_go_tan", "oracle_go_sin", "oracle_go_cos"):
+            getattr(l, fn).argtypes = [C.c_double]
+            getattr(l, fn).restype = C.c_double
+        l.oracle_pcg_float64.argtypes = [C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+        l.oracle_pcg_float64.restype = None
+        _lib = l
+    return _lib
+
+
+def render_rows(packed, y0=0, y1=None, threads=8):
+    """Oracle render of rows [y0, y1): returns (uint8[rows, W, 4], rt_stats)."""
+    from importlib import import_module
+    abi = import_module("go_raytracer_amd.abi")
+    if y1 is None:
+        y1 = packed.height
+    out = np.zeros((y1 - y0, packed.width, 4), dtype=np.uint8)
+    st = abi.rt_stats()
+    rc = lib().oracle_render_rows(C.addressof(packed.scene), y0, y1, threads,
+                                  out.ctypes.data_as(C.c_void_p), C.addressof(st))
+    if rc != 0:
+        raise RuntimeError("oracle_render_rows failed: %d" % rc)
+    return out, st
