@@ -1,0 +1,1085 @@
+// rt_kernel.hip -- MI355X (gfx950) megakernel for the GML raytracer hot path
+// plus the C ABI of include/rt_abi.h.
+//
+// Replaces (timdestan/go-raytracer):
+//   raytracer.go:589-682  Render: camera, PCG jitter, 4-sample AA, quantise
+//   raytracer.go:469-562  closestHit / traceRay (recursion -> explicit stack)
+//   raytracer.go:372-467  computeLighting / inShadow / refract / fresnel
+//   raytracer.go:51-370   Sphere/Plane/Cube/Cylinder Intersect + surface props
+//   raytracer.go:724-830  scene conversion (host side, below)
+//
+// Execution model: persistent wave64 workgroups. Each LANE owns one pixel at
+// a time and runs the reference's recursion as a state machine over an
+// explicit per-lane frame stack (lane-interleaved in HBM, so pushes/pops are
+// coalesced). Waves refill idle lanes from a per-wave pool of 64 contiguous
+// pixels (one 8x8 tile) taken from a global atomic queue -- the analogue of
+// the reference's channel of (column, 20-row) work items
+// (raytracer.go:611-677) with per-lane granularity. Object loops are
+// wave-uniform (brute force over the flattened object list, exactly like
+// closestHit), so object records are fetched with scalar loads and the
+// primitive-kind switch never diverges.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_abi.h"
+#include "rt_device.h"
+
+using namespace rt;
+
+// ---------------------------------------------------------------------------
+// Device scene layout (built by rt_set_scene; doubles unless stated)
+// geo   [nobj][GEO]   0..11 WorldToObject rows 0-2 (prim.Mat4 affine part)
+//                     12..14 plane normal (object space), 15 plane D
+// shade [nobj][SHD]   0..11 ObjectToWorld rows 0-2, 12..29 NormalWorld per face
+// mats  [nmat][MAT]   0..2 colour, 3 reflectivity, 4..5 baked fuzz offset
+//                     (fuzz*cos^2, fuzz*sin^2; raytracer.go:517-521), 6 fuzz>=0,
+//                     7 transparency, 8 ior, 9 kd, 10 ks, 11 specular exponent
+// kind  [nobj] int32; objmat [nobj][8] int32 per-face material index
+// lights[nl][8]       0..2 position, 3..5 colour
+// ---------------------------------------------------------------------------
+enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8 };
+enum { FRAME_FIELDS = 14 };  // Lw[3] cfirst[3] pend_o[3] pend_d[3] kr packed
+enum { CHUNK = 64, TILE = 8 };
+enum {
+  ST_PRIMARY = 0, ST_SECONDARY = 1, ST_SHADOW = 2, ST_TRACED = 3, ST_STESTS = 4,  // 4 kinds
+  ST_SHADED = 8, ST_COUNT = 9
+};
+
+struct Params {
+  const double* __restrict__ geo;
+  const int* __restrict__ kind;
+  const double* __restrict__ shade;
+  const int* __restrict__ objmat;
+  const double* __restrict__ mats;
+  const double* __restrict__ lights;
+  const uint64_t* __restrict__ jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
+  unsigned int* queue;
+  unsigned long long* stats;
+  double* stack;
+  uint32_t* out;
+  int width, height, depth, nobj, nlights, y0, y1, tiles_x;
+  unsigned int total_slots;
+  int frames;  // stack frames per lane (depth - 1, >= 1)
+  double vw, vh;
+  double amb[3], bg0[3], bg1[3];
+  double cube_n[6][3];
+  double cube_d[6];
+};
+
+struct Ray {
+  d3 o, d;
+};
+
+// rayToObjectSpace (raytracer.go:51-56) with prim.Mat4.MulPoint/MulDir
+// (vec.go:298-313): m points at the 3x4 affine rows.
+__device__ __forceinline__ Ray to_obj(const double* __restrict__ m, const Ray& r) {
+  Ray l;
+  l.o = mk(m[0] * r.o.x + m[1] * r.o.y + m[2] * r.o.z + m[3],
+           m[4] * r.o.x + m[5] * r.o.y + m[6] * r.o.z + m[7],
+           m[8] * r.o.x + m[9] * r.o.y + m[10] * r.o.z + m[11]);
+  l.d = mk(m[0] * r.d.x + m[1] * r.d.y + m[2] * r.d.z,
+           m[4] * r.d.x + m[5] * r.d.y + m[6] * r.d.z,
+           m[8] * r.d.x + m[9] * r.d.y + m[10] * r.d.z);
+  return l;
+}
+
+// Sphere.Intersect (raytracer.go:58-104): unit sphere, near root only.
+__device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
+  double a = dot(l.d, l.d);
+  double hb = dot(l.o, l.d);
+  double c = dot(l.o, l.o) - 1.0;
+  double disc = hb * hb - a * c;
+  if (disc < 0.0) return false;
+  double sq = __builtin_sqrt(disc);
+  double t0 = (-hb - sq) / a;
+  if (t0 > 0.0) {
+    t = t0;
+    return true;
+  }
+  return false;
+}
+
+// Plane.Intersect (raytracer.go:164-180) on an object-space ray.
+__device__ __forceinline__ bool plane_hit(const Ray& l, d3 n, double pd, double& t) {
+  double denom = dot(n, l.d);
+  if (__builtin_fabs(denom) < 1e-6) return false;
+  double tt = (-pd - dot(n, l.o)) / denom;
+  if (tt <= 0.0) return false;
+  t = tt;
+  return true;
+}
+
+// Cube.Intersect (raytracer.go:214-240): 6 faces; every face re-transforms the
+// ray with the same matrix in the reference, so one transform is identical.
+__device__ __forceinline__ bool cube_hit(const Params& P, const Ray& l, double& t, int& face) {
+  bool found = false;
+  double best = 0.0;
+  int bf = 0;
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    double ft;
+    d3 n = mk(P.cube_n[f][0], P.cube_n[f][1], P.cube_n[f][2]);
+    if (!plane_hit(l, n, P.cube_d[f], ft)) continue;
+    if (ft < 0.0) continue;
+    d3 p = add(l.o, scale(l.d, ft));
+    if (p.x < 0 || p.x > 1 || p.y < 0 || p.y > 1 || p.z < 0 || p.z > 1) continue;
+    if (!found || ft < best) {
+      found = true;
+      best = ft;
+      bf = f;
+    }
+  }
+  if (found) {
+    t = best;
+    face = bf;
+  }
+  return found;
+}
+
+// Cylinder.Intersect (raytracer.go:279-337).
+__device__ __forceinline__ bool cylinder_hit(const Ray& l, double& t, int& face) {
+  double bestT = __builtin_inf();
+  int bestFace = -1;
+  double a = l.d.x * l.d.x + l.d.z * l.d.z;
+  if (a > 1e-12) {
+    double hb = l.o.x * l.d.x + l.o.z * l.d.z;
+    double c0 = l.o.x * l.o.x + l.o.z * l.o.z - 1.0;
+    double disc = hb * hb - a * c0;
+    if (disc >= 0.0) {
+      double sq = __builtin_sqrt(disc);
+      double t0 = (-hb - sq) / a;
+      double t1 = (-hb + sq) / a;
+      double y0 = l.o.y + l.d.y * t0;
+      if (y0 >= 0.0 && y0 <= 1.0 && t0 > 0.0 && t0 < bestT) {
+        bestT = t0;
+        bestFace = 0;
+      }
+      double y1 = l.o.y + l.d.y * t1;
+      if (y1 >= 0.0 && y1 <= 1.0 && t1 > 0.0 && t1 < bestT) {
+        bestT = t1;
+        bestFace = 0;
+      }
+    }
+  }
+  if (__builtin_fabs(l.d.y) > 1e-12) {
+    double tTop = (1.0 - l.o.y) / l.d.y;
+    double px = l.o.x + l.d.x * tTop, pz = l.o.z + l.d.z * tTop;
+    if (px * px + pz * pz <= 1.0 && tTop > 0.0 && tTop < bestT) {
+      bestT = tTop;
+      bestFace = 1;
+    }
+    double tBot = -l.o.y / l.d.y;
+    px = l.o.x + l.d.x * tBot;
+    pz = l.o.z + l.d.z * tBot;
+    if (px * px + pz * pz <= 1.0 && tBot > 0.0 && tBot < bestT) {
+      bestT = tBot;
+      bestFace = 2;
+    }
+  }
+  if (bestFace < 0) return false;
+  t = bestT;
+  face = bestFace;
+  return true;
+}
+
+// One SceneObject.Intersect on a world-space ray; kind is wave-uniform.
+__device__ __forceinline__ bool object_hit(const Params& P, int k, const double* __restrict__ g, const Ray& r,
+                                           double& t, int& face) {
+  Ray l = to_obj(g, r);
+  face = 0;
+  switch (k) {
+    case RT_SPHERE:
+      return sphere_hit(l, t);
+    case RT_PLANE:
+      return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
+    case RT_CUBE:
+      return cube_hit(P, l, t, face);
+    default:
+      return cylinder_hit(l, t, face);
+  }
+}
+
+__device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(__ballot(b)); }
+
+// Frame stack: lane-interleaved so that one field of one frame is a
+// contiguous 512-B row for the wave.
+__device__ __forceinline__ double* frame_ptr(double* base, int frame) { return base + (size_t)frame * FRAME_FIELDS * 64; }
+__device__ __forceinline__ void st3(double* f, int field, d3 v) {
+  f[(field + 0) * 64] = v.x;
+  f[(field + 1) * 64] = v.y;
+  f[(field + 2) * 64] = v.z;
+}
+__device__ __forceinline__ d3 ld3(const double* f, int field) {
+  return mk(f[(field + 0) * 64], f[(field + 1) * 64], f[(field + 2) * 64]);
+}
+
+// Frame flags (packed with the material index).
+enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8 };
+
+// traceRay's final combine (raytracer.go:557-561).
+__device__ __forceinline__ d3 combine(bool tmode, d3 lw, d3 col, double refl, double kr, d3 R, d3 Tr) {
+  if (!tmode) return clamp(mul(add(lw, scale(R, refl)), col));
+  return clamp(mul(add(lw, add(scale(R, kr), scale(Tr, 1.0 - kr))), col));
+}
+
+__global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
+  const int lane = (int)__lane_id();
+  double* stk = P.stack + (size_t)blockIdx.x * ((size_t)P.frames * FRAME_FIELDS * 64) + lane;
+  const d3 eye = mk(0.0, 0.0, -1.0);  // raytracer.go:605-609
+
+  // lane state
+  bool alive = false;
+  int px = 0, py = 0, sample = 0, sp = 0;
+  Pcg rng{0, 0};
+  d3 sum = mk(0, 0, 0);
+  Ray ray;
+  ray.o = mk(0, 0, 0);
+  ray.d = mk(0, 0, 1);
+
+  // wave-uniform pool and counters
+  unsigned int pool_next = 0, pool_end = 0;
+  bool exhausted = false;
+  uint64_t c_primary = 0, c_secondary = 0, c_shadow = 0, c_traced = 0, c_shaded = 0;
+  uint64_t c_stest[4] = {0, 0, 0, 0};
+
+  const double W1 = (double)(P.width - 1), H1 = (double)(P.height - 1);
+
+  // New sample ray: raytracer.go:642-649.
+  auto gen_ray = [&]() {
+    double dx = pcg_float64(rng) - 0.5;
+    double dy = pcg_float64(rng) - 0.5;
+    double u = ((double)px + dx) / W1 * P.vw - P.vw / 2.0;
+    double v = ((double)py + dy) / H1 * P.vh - P.vh / 2.0;
+    ray.o = mk(u, -v, 0.0);
+    ray.d = norm(sub(ray.o, eye));
+  };
+
+  for (;;) {
+    // ---- refill idle lanes from the wave pool (one 8x8 tile per chunk) ----
+    for (;;) {
+      bool need = !alive;
+      uint64_t mask = __ballot(need);
+      if (mask == 0 || exhausted) break;
+      if (pool_next >= pool_end) {
+        unsigned int base = 0;
+        if (lane == 0) base = atomicAdd(P.queue, (unsigned int)CHUNK);
+        base = __shfl(base, 0);
+        if (base >= P.total_slots) {
+          exhausted = true;
+          break;
+        }
+        pool_next = base;
+        pool_end = min(base + (unsigned int)CHUNK, P.total_slots);
+      }
+      unsigned int rank = __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
+      unsigned int navail = pool_end - pool_next;
+      unsigned int take = min((unsigned int)__popcll(mask), navail);
+      if (need && rank < take) {
+        unsigned int slot = pool_next + rank;
+        unsigned int tile = slot / (TILE * TILE), within = slot % (TILE * TILE);
+        int x = (int)((tile % (unsigned)P.tiles_x) * TILE + within % TILE);
+        int y = P.y0 + (int)((tile / (unsigned)P.tiles_x) * TILE + within / TILE);
+        if (x < P.width && y < P.y1) {
+          px = x;
+          py = y;
+          // rng = PCG(0xDEAD^x, 0xBEEF^ymin) advanced 8*(y%20) draws
+          // (raytracer.go:632-643: 2 draws per sample, 4 samples per row).
+          int ymin = y - y % 20;
+          Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
+          const uint64_t* j = P.jump + (size_t)(y % 20) * 4;
+          rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
+          sample = 0;
+          sum = mk(0, 0, 0);
+          sp = 0;
+          gen_ray();
+          alive = true;
+        }
+      }
+      pool_next += take;
+    }
+    if (!__any(alive)) break;
+    c_primary += 0;  // primaries are counted when generated (below)
+
+    // ---- closestHit over all objects (raytracer.go:469-483) ----
+    bool found = false;
+    double best_t = 0.0;
+    int best_i = 0, best_f = 0;
+    for (int i = 0; i < P.nobj; i++) {
+      const int k = P.kind[i];
+      const double* g = P.geo + (size_t)i * GEO;
+      if (alive) {
+        double t;
+        int f;
+        if (object_hit(P, k, g, ray, t, f)) {
+          if (!found || t < best_t) {
+            found = true;
+            best_t = t;
+            best_i = i;
+            best_f = f;
+          }
+        }
+      }
+    }
+    c_traced += popc_ballot(alive);
+
+    bool have_res = false;
+    d3 res = mk(0, 0, 0);
+    if (alive && !found) {  // background gradient, raytracer.go:493-497
+      double t = 0.5 * (ray.d.y + 1.0);
+      res = lerp(mk(P.bg0[0], P.bg0[1], P.bg0[2]), mk(P.bg1[0], P.bg1[1], P.bg1[2]), t);
+      have_res = true;
+    }
+    const bool hit = alive && found;
+    c_shaded += popc_ballot(hit);
+
+    // ---- ComputeSurfaceProps (raytracer.go:106-122, 182-194, 242-260, 339-370) ----
+    d3 pw = mk(0, 0, 0), nw = mk(0, 0, 1);
+    int mat = 0;
+    if (hit) {
+      const double* g = P.geo + (size_t)best_i * GEO;
+      const double* s = P.shade + (size_t)best_i * SHD;
+      const int k = P.kind[best_i];
+      Ray l = to_obj(g, ray);
+      d3 p = add(l.o, scale(l.d, best_t));  // Hit.PointObj
+      pw = mk(s[0] * p.x + s[1] * p.y + s[2] * p.z + s[3], s[4] * p.x + s[5] * p.y + s[6] * p.z + s[7],
+              s[8] * p.x + s[9] * p.y + s[10] * p.z + s[11]);
+      if (k == RT_SPHERE) {
+        nw = p;
+      } else if (k == RT_CYLINDER) {
+        d3 n = best_f == 0 ? mk(p.x, 0, p.z) : (best_f == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
+        // NormalMat = WorldToObject^T (raytracer.go:814): MulDir then Normalize.
+        nw = norm(mk(g[0] * n.x + g[4] * n.y + g[8] * n.z, g[1] * n.x + g[5] * n.y + g[9] * n.z,
+                     g[2] * n.x + g[6] * n.y + g[10] * n.z));
+      } else {
+        nw = mk(s[12 + best_f * 3], s[13 + best_f * 3], s[14 + best_f * 3]);
+      }
+      mat = P.objmat[(size_t)best_i * OMAT + best_f];
+    }
+
+    // ---- computeLighting + inShadow (raytracer.go:372-429) ----
+    d3 L = mk(0, 0, 0);
+    const double* M = P.mats + (size_t)mat * MAT;
+    if (hit) L = scale(mk(P.amb[0], P.amb[1], P.amb[2]), M[9]);
+    const double rlen = len(ray.d);
+    const d3 sorig = add(pw, scale(nw, 1e-4));
+    for (int li = 0; li < P.nlights; li++) {
+      const double* lt = P.lights + (size_t)li * LGT;
+      d3 lpos = mk(lt[0], lt[1], lt[2]);
+      d3 lth = sub(lpos, pw);
+      double dist = len(lth);
+      d3 ldir = norm(lth);
+      c_shadow += popc_ballot(hit);
+      bool open = hit;  // lanes still looking for an occluder
+      Ray sr;
+      sr.o = sorig;
+      sr.d = ldir;
+      for (int i = 0; i < P.nobj; i++) {
+        if (!__any(open)) break;
+        const int k = P.kind[i];
+        const double* g = P.geo + (size_t)i * GEO;
+        bool test = open && i != best_i;
+        c_stest[k] += popc_ballot(test);
+        if (test) {
+          double t;
+          int f;
+          if (object_hit(P, k, g, sr, t, f)) {
+            if (t * rlen < dist) open = false;
+          }
+        }
+      }
+      bool lit = hit && open;
+      if (lit) {
+        d3 lcol = mk(lt[3], lt[4], lt[5]);
+        double ndl = go_max(0, dot(nw, ldir));
+        d3 diffuse = scale(lcol, ndl * M[9]);
+        d3 H = norm(add(neg(ray.d), ldir));
+        double spec = go_max(0, dot(nw, H));
+        d3 specular = scale(lcol, M[10] * go_pow(spec, M[11]));
+        L = add(add(L, diffuse), specular);
+      }
+    }
+
+    // ---- traceRay body after lighting (raytracer.go:505-561) ----
+    if (hit) {
+      d3 col = mk(M[0], M[1], M[2]);
+      double refl = M[3], T = M[7];
+      if (refl == 0 && T == 0) {
+        res = clamp(mul(L, col));
+        have_res = true;
+      } else {
+        bool hasR = refl > 0;
+        Ray rr;
+        rr.o = mk(0, 0, 0);
+        rr.d = mk(0, 0, 1);
+        if (hasR) {
+          d3 rd = sub(ray.d, scale(nw, 2.0 * dot(ray.d, nw)));
+          if (M[6] != 0.0) rd = add(rd, mk(M[4], M[5], 0.0));
+          rr.o = add(pw, scale(nw, 1e-4));
+          rr.d = norm(rd);
+        }
+        bool tmode = T > 0;
+        bool hasT = false;
+        Ray tr;
+        tr.o = mk(0, 0, 0);
+        tr.d = mk(0, 0, 1);
+        double kr = 0.0;
+        d3 lw = L;
+        if (tmode) {
+          double n1 = 1.0, n2 = M[8];
+          d3 nn = nw;
+          if (dot(ray.d, nn) > 0.0) {
+            n1 = M[8];
+            n2 = 1.0;
+            nn = scale(nn, -1.0);
+          }
+          // refract (raytracer.go:438-450)
+          double ratio = n1 / n2;
+          double cosI = -dot(nn, ray.d);
+          double sinT2 = ratio * ratio * (1.0 - cosI * cosI);
+          if (!(sinT2 > 1.0)) {
+            double cosT = __builtin_sqrt(1.0 - sinT2);
+            d3 td = add(scale(ray.d, ratio), scale(nn, ratio * cosI - cosT));
+            if (!iszero(td)) {
+              hasT = true;
+              tr.o = sub(pw, scale(nn, 1e-4));
+              tr.d = td;
+            }
+          }
+          // fresnel (raytracer.go:456-467) on the unflipped normal
+          double cosi = dot(ray.d, nw) / (len(ray.d) * len(nw));
+          double r0 = (1.0 - M[8]) / (1.0 + M[8]);
+          r0 = r0 * r0;
+          double cost = __builtin_fabs(cosi);
+          kr = r0 + (1 - r0) * go_pow(1 - cost, 5);
+          lw = scale(L, 1.0 - T);
+        }
+        const int d = P.depth - sp;  // depth of the current ray
+        if (d - 1 > 0 && (hasR || hasT)) {
+          double* f = frame_ptr(stk, sp);
+          st3(f, 0, lw);
+          if (hasR && hasT) {
+            st3(f, 6, tr.o);
+            st3(f, 9, tr.d);
+          }
+          f[12 * 64] = kr;
+          long long packed = ((long long)mat << 8) | (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
+          f[13 * 64] = __longlong_as_double(packed);
+          sp++;
+          ray = hasR ? rr : tr;
+        } else {
+          res = combine(tmode, lw, col, refl, kr, mk(0, 0, 0), mk(0, 0, 0));
+          have_res = true;
+        }
+      }
+    }
+    // lanes that pushed a frame trace a secondary ray next iteration
+    c_secondary += popc_ballot(hit && !have_res);
+
+    // ---- unwind: propagate results up the frame stack (post-order) ----
+    while (__any(have_res)) {
+      if (have_res) {
+        if (sp == 0) {
+          sum = add(sum, res);  // raytracer.go:651
+          sample++;
+          if (sample == 4) {
+            d3 c = scale(sum, 1.0 / 4.0);  // raytracer.go:656 -> vec.go:104-107
+            uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
+            uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
+            uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
+            P.out[(size_t)(py - P.y0) * (size_t)P.width + (size_t)px] =
+                (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+            alive = false;
+          } else {
+            gen_ray();
+          }
+          have_res = false;
+        } else {
+          double* f = frame_ptr(stk, sp - 1);
+          long long packed = __double_as_longlong(f[13 * 64]);
+          int fl = (int)(packed & 0xff);
+          int fm = (int)(packed >> 8);
+          if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
+            // reflection child done; trace the pending refraction child
+            st3(f, 3, res);
+            f[13 * 64] = __longlong_as_double(packed | FL_STAGE);
+            ray.o = ld3(f, 6);
+            ray.d = ld3(f, 9);
+            have_res = false;
+          } else {
+            const double* FM = P.mats + (size_t)fm * MAT;
+            d3 R = mk(0, 0, 0), Tr = mk(0, 0, 0);
+            if ((fl & FL_HASR) && (fl & FL_HAST)) {
+              R = ld3(f, 3);
+              Tr = res;
+            } else if (fl & FL_HASR) {
+              R = res;
+            } else {
+              Tr = res;
+            }
+            res = combine((fl & FL_TMODE) != 0, ld3(f, 0), mk(FM[0], FM[1], FM[2]), FM[3], f[12 * 64], R, Tr);
+            sp--;
+          }
+        }
+      }
+    }
+    c_secondary += 0;
+    // count lanes that started a pending refraction child or a new sample
+  }
+
+  // primaries are exactly 4 per pixel; secondaries = traced - primaries
+  if (lane == 0) {
+    atomicAdd(P.stats + ST_TRACED, (unsigned long long)c_traced);
+    atomicAdd(P.stats + ST_SHADOW, (unsigned long long)c_shadow);
+    atomicAdd(P.stats + ST_SHADED, (unsigned long long)c_shaded);
+    for (int k = 0; k < 4; k++) atomicAdd(P.stats + ST_STESTS + k, (unsigned long long)c_stest[k]);
+  }
+}
+
+// ===========================================================================
+// Host side: scene conversion (raytracer.go:724-830) and the C ABI
+// ===========================================================================
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(RT_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct M4 {
+  double m[4][4];
+};
+
+M4 ident() {
+  M4 r;
+  std::memset(&r, 0, sizeof r);
+  r.m[0][0] = r.m[1][1] = r.m[2][2] = r.m[3][3] = 1.0;
+  return r;
+}
+
+// prim.Mat4.Inverse (vec.go:319-365)
+bool inverse(const M4& M, M4& inv) {
+  const double(*m)[4] = M.m;
+  double a = m[0][0], b = m[0][1], c = m[0][2];
+  double d = m[1][0], e = m[1][1], f = m[1][2];
+  double g = m[2][0], h = m[2][1], i = m[2][2];
+  double det = a * (e * i - f * h) - b * (d * i - f * g) + c * (d * h - e * g);
+  if (det == 0.0) return false;
+  inv.m[0][0] = (e * i - f * h) / det;
+  inv.m[0][1] = (c * h - b * i) / det;
+  inv.m[0][2] = (b * f - c * e) / det;
+  inv.m[1][0] = (f * g - d * i) / det;
+  inv.m[1][1] = (a * i - c * g) / det;
+  inv.m[1][2] = (c * d - a * f) / det;
+  inv.m[2][0] = (d * h - e * g) / det;
+  inv.m[2][1] = (b * g - a * h) / det;
+  inv.m[2][2] = (a * e - b * d) / det;
+  inv.m[3][0] = inv.m[3][1] = inv.m[3][2] = 0.0;
+  inv.m[3][3] = 1.0;
+  inv.m[0][3] = -(inv.m[0][0] * m[0][3] + inv.m[0][1] * m[1][3] + inv.m[0][2] * m[2][3]);
+  inv.m[1][3] = -(inv.m[1][0] * m[0][3] + inv.m[1][1] * m[1][3] + inv.m[1][2] * m[2][3]);
+  inv.m[2][3] = -(inv.m[2][0] * m[0][3] + inv.m[2][1] * m[1][3] + inv.m[2][2] * m[2][3]);
+  return true;
+}
+
+// createPlane's NormalWorld = WorldToObject^T.MulDir(normal).Normalize() and
+// D = -normal.Dot(point) (raytracer.go:764-774).
+void plane_consts(const M4& w2o, const double pt[3], const double n[3], double nw[3], double* dval) {
+  // Transpose then MulDir: row i of W2O^T is column i of W2O.
+  double x = w2o.m[0][0] * n[0] + w2o.m[1][0] * n[1] + w2o.m[2][0] * n[2];
+  double y = w2o.m[0][1] * n[0] + w2o.m[1][1] * n[1] + w2o.m[2][1] * n[2];
+  double z = w2o.m[0][2] * n[0] + w2o.m[1][2] * n[1] + w2o.m[2][2] * n[2];
+  double mag = std::sqrt(x * x + y * y + z * z);
+  nw[0] = x / mag;
+  nw[1] = y / mag;
+  nw[2] = z / mag;
+  *dval = -(n[0] * pt[0] + n[1] * pt[1] + n[2] * pt[2]);
+}
+
+// prim.PlanesForUnitCube (internal/prim/plane.go:29-38)
+const double kCubePt[6][3] = {{0, 0, 0}, {0, 0, 1}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 0}};
+const double kCubeN[6][3] = {{0, 0, -1}, {0, 0, 1}, {-1, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, -1, 0}};
+
+// Go math.Tan (tan.go), Sin/Cos (sin.go): Cephes, Cody-Waite reduction.
+const double kSin[6] = {1.58962301576546568060e-10, -2.50507477628578072866e-8, 2.75573136213857245213e-6,
+                        -1.98412698295895385996e-4, 8.33333333332211858878e-3, -1.66666666666666307295e-1};
+const double kCos[6] = {-1.13585365213876817300e-11, 2.08757008419747316778e-9, -2.75573141792967388112e-7,
+                        2.48015872888517045348e-5,   -1.38888888888730564116e-3, 4.16666666666665929218e-2};
+const double kPI4A = 7.85398125648498535156e-1, kPI4B = 3.77489470793079817668e-8,
+             kPI4C = 2.69515142907905952645e-15, k4OverPi = 1.2732395447351628;
+
+double poly_sin(double z, double zz) {
+  return z + z * zz * ((((((kSin[0] * zz) + kSin[1]) * zz + kSin[2]) * zz + kSin[3]) * zz + kSin[4]) * zz + kSin[5]);
+}
+double poly_cos(double zz) {
+  return 1.0 - 0.5 * zz + zz * zz * ((((((kCos[0] * zz) + kCos[1]) * zz + kCos[2]) * zz + kCos[3]) * zz + kCos[4]) * zz + kCos[5]);
+}
+bool reduce(double x, uint64_t& j, double& z) {  // x >= 0
+  if (x >= (double)(1 << 29)) return false;        // Payne-Hanek range: not restated
+  j = (uint64_t)(x * k4OverPi);
+  double y = (double)j;
+  if (j & 1) {
+    j++;
+    y++;
+  }
+  z = ((x - y * kPI4A) - y * kPI4B) - y * kPI4C;
+  return true;
+}
+bool go_sin(double x, double& out) {
+  if (x == 0 || std::isnan(x)) { out = x; return true; }
+  if (std::isinf(x)) { out = NAN; return true; }
+  bool sign = false;
+  if (x < 0) { x = -x; sign = true; }
+  uint64_t j;
+  double z;
+  if (!reduce(x, j, z)) return false;
+  j &= 7;
+  if (j > 3) { sign = !sign; j -= 4; }
+  double zz = z * z;
+  double y = (j == 1 || j == 2) ? poly_cos(zz) : poly_sin(z, zz);
+  out = sign ? -y : y;
+  return true;
+}
+bool go_cos(double x, double& out) {
+  if (std::isnan(x) || std::isinf(x)) { out = NAN; return true; }
+  bool sign = false;
+  x = std::fabs(x);
+  uint64_t j;
+  double z;
+  if (!reduce(x, j, z)) return false;
+  j &= 7;
+  if (j > 3) { j -= 4; sign = !sign; }
+  if (j > 1) sign = !sign;
+  double zz = z * z;
+  double y = (j == 1 || j == 2) ? poly_sin(z, zz) : poly_cos(zz);
+  out = sign ? -y : y;
+  return true;
+}
+bool go_tan(double x, double& out) {
+  static const double P[3] = {-1.30936939181383777646e4, 1.15351664838587416140e6, -1.79565251976484877988e7};
+  static const double Q[5] = {1.0, 1.36812963470692954678e4, -1.32089234440210967447e6, 2.50083801823357915839e7,
+                              -5.38695755929454629881e7};
+  if (x == 0 || std::isnan(x)) { out = x; return true; }
+  if (std::isinf(x)) { out = NAN; return true; }
+  bool sign = false;
+  if (x < 0) { x = -x; sign = true; }
+  uint64_t j;
+  double z;
+  if (!reduce(x, j, z)) return false;
+  double zz = z * z;
+  double y;
+  if (zz > 1e-14)
+    y = z + z * (zz * (((P[0] * zz) + P[1]) * zz + P[2]) / ((((zz + Q[1]) * zz + Q[2]) * zz + Q[3]) * zz + Q[4]));
+  else
+    y = z;
+  if (j & 2) y = -1 / y;
+  out = sign ? -y : y;
+  return true;
+}
+
+struct DevScene {
+  int width = 0, height = 0, depth = 0, nobj = 0, nlights = 0, nmats = 0;
+  double vw = 0, vh = 0;
+  double amb[3] = {0, 0, 0}, bg0[3] = {0, 0, 0}, bg1[3] = {0, 0, 0};
+  double* geo = nullptr;
+  int* kind = nullptr;
+  double* shade = nullptr;
+  int* objmat = nullptr;
+  double* mats = nullptr;
+  double* lights = nullptr;
+};
+
+}  // namespace
+
+struct rt_context {
+  int device = 0;
+  int cus = 0;
+  int grid = 0;
+  DevScene sc;
+  bool has_scene = false;
+  uint64_t* jump = nullptr;
+  unsigned int* queue = nullptr;
+  unsigned long long* stats = nullptr;
+  double* stack = nullptr;
+  size_t stack_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  uint64_t primary_pending = 0;  // host-side count of launched primary rays
+  double cube_n[6][3];
+  double cube_d[6];
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+void free_scene(DevScene& s) {
+  (void)hipFree(s.geo);
+  (void)hipFree(s.kind);
+  (void)hipFree(s.shade);
+  (void)hipFree(s.objmat);
+  (void)hipFree(s.mats);
+  (void)hipFree(s.lights);
+  s = DevScene();
+}
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src) {
+  size_t bytes = std::max<size_t>(1, src.size()) * sizeof(T);
+  HIP_TRY(hipMalloc((void**)dst, bytes));
+  if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_create(int device, rt_context** out) {
+  if (!out) return fail(RT_E_INVALID, "rt_create: out is NULL");
+  *out = nullptr;
+  if (device < 0) HIP_TRY(hipGetDevice(&device));
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device >= ndev) return fail(RT_E_INVALID, "rt_create: device index out of range");
+  DeviceGuard guard(device);
+  rt_context* c = new rt_context();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    delete c;
+    return fail(RT_E_DEVICE, "hipGetDeviceProperties failed");
+  }
+  c->cus = prop.multiProcessorCount;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel, 64, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 8;
+  c->grid = c->cus * std::min(per_cu, 32);
+  // PCG jump table: 8*r LCG steps, r = 0..19 (pcg.go: mul/inc constants).
+  std::vector<uint64_t> jump(20 * 4);
+  {
+    typedef unsigned __int128 u128;
+    const u128 mul = ((u128)2549297995355413924ULL << 64) | 4865540595714422341ULL;
+    const u128 inc = ((u128)6364136223846793005ULL << 64) | 1442695040888963407ULL;
+    u128 A = 1, Cc = 0;
+    for (int step = 0; step <= 8 * 19; step++) {
+      if (step % 8 == 0) {
+        int r = step / 8;
+        jump[r * 4 + 0] = (uint64_t)(A >> 64);
+        jump[r * 4 + 1] = (uint64_t)A;
+        jump[r * 4 + 2] = (uint64_t)(Cc >> 64);
+        jump[r * 4 + 3] = (uint64_t)Cc;
+      }
+      A = A * mul;
+      Cc = Cc * mul + inc;
+    }
+  }
+  int rc = upload(&c->jump, jump);
+  if (rc == RT_OK && hipMalloc((void**)&c->queue, 256) != hipSuccess) rc = fail(RT_E_NOMEM, "queue alloc");
+  if (rc == RT_OK && hipMalloc((void**)&c->stats, sizeof(unsigned long long) * 64) != hipSuccess)
+    rc = fail(RT_E_NOMEM, "stats alloc");
+  if (rc == RT_OK && hipMemset(c->stats, 0, sizeof(unsigned long long) * 64) != hipSuccess)
+    rc = fail(RT_E_DEVICE, "stats memset");
+  if (rc == RT_OK && (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess))
+    rc = fail(RT_E_DEVICE, "event create");
+  // Cube face planes: normal and D = -normal.Dot(point), same op order as Go.
+  for (int f = 0; f < 6; f++) {
+    for (int k = 0; k < 3; k++) c->cube_n[f][k] = kCubeN[f][k];
+    c->cube_d[f] = -(kCubeN[f][0] * kCubePt[f][0] + kCubeN[f][1] * kCubePt[f][1] + kCubeN[f][2] * kCubePt[f][2]);
+  }
+  if (rc != RT_OK) {
+    rt_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+void rt_destroy(rt_context* c) {
+  if (!c) return;
+  DeviceGuard guard(c->device);
+  free_scene(c->sc);
+  (void)hipFree(c->jump);
+  (void)hipFree(c->queue);
+  (void)hipFree(c->stats);
+  (void)hipFree(c->stack);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+}
+
+int rt_set_scene(rt_context* c, const rt_scene* in) {
+  if (!c || !in) return fail(RT_E_INVALID, "rt_set_scene: NULL argument");
+  if (in->width <= 1 || in->height <= 1) return fail(RT_E_INVALID, "rt_set_scene: width/height must be > 1");
+  if (in->num_objects < 0 || in->num_lights < 0 || in->num_materials <= 0)
+    return fail(RT_E_INVALID, "rt_set_scene: negative counts or no materials");
+  if ((in->num_objects > 0 && !in->objects) || (in->num_lights > 0 && !in->lights) || !in->materials)
+    return fail(RT_E_INVALID, "rt_set_scene: NULL array");
+  DeviceGuard guard(c->device);
+  DevScene s;
+  s.width = in->width;
+  s.height = in->height;
+  s.depth = in->depth <= 0 ? 3 : in->depth;                  // raytracer.go:592-595
+  double fov = in->fov <= 0.0 ? 90.0 : in->fov;              // raytracer.go:597-600
+  double fovr = fov * M_PI / 180.0;                          // :601
+  double tn;
+  if (!go_tan(fovr / 2.0, tn)) return fail(RT_E_INVALID, "fov outside the restated math.Tan range");
+  s.vw = 2.0 / tn;                                           // :602
+  s.vh = s.vw * ((double)in->height / (double)in->width);    // :603
+  for (int k = 0; k < 3; k++) {
+    s.amb[k] = in->ambient[k];
+    s.bg0[k] = in->bg_start[k];
+    s.bg1[k] = in->bg_end[k];
+  }
+  s.nobj = in->num_objects;
+  s.nlights = in->num_lights;
+  s.nmats = in->num_materials;
+
+  std::vector<double> geo((size_t)s.nobj * GEO, 0.0), shade((size_t)s.nobj * SHD, 0.0);
+  std::vector<int> kind(s.nobj), objmat((size_t)s.nobj * OMAT, 0);
+  for (int i = 0; i < s.nobj; i++) {
+    const rt_object& o = in->objects[i];
+    if (o.kind < 0 || o.kind >= RT_NUM_KINDS) return fail(RT_E_INVALID, "unknown scene object type");
+    kind[i] = o.kind;
+    for (int f = 0; f < RT_MAX_FACES; f++) {
+      if (o.material[f] < 0 || o.material[f] >= in->num_materials)
+        return fail(RT_E_INVALID, "material index out of range");
+      objmat[(size_t)i * OMAT + f] = o.material[f];
+    }
+    M4 o2w = ident(), w2o = ident();  // raytracer.go:757-762
+    if (o.has_transform) {
+      std::memcpy(o2w.m, o.transform, sizeof(double) * 16);
+      if (!inverse(o2w, w2o)) return fail(RT_E_SINGULAR, "object transform is singular (det == 0)");
+    }
+    double* g = &geo[(size_t)i * GEO];
+    double* sh = &shade[(size_t)i * SHD];
+    for (int r = 0; r < 3; r++)
+      for (int k = 0; k < 4; k++) {
+        g[r * 4 + k] = w2o.m[r][k];
+        sh[r * 4 + k] = o2w.m[r][k];
+      }
+    if (o.kind == RT_PLANE) {
+      double nw[3], dv;
+      plane_consts(w2o, o.plane_point, o.plane_normal, nw, &dv);
+      g[12] = o.plane_normal[0];
+      g[13] = o.plane_normal[1];
+      g[14] = o.plane_normal[2];
+      g[15] = dv;
+      for (int k = 0; k < 3; k++) sh[12 + k] = nw[k];
+    } else if (o.kind == RT_CUBE) {
+      for (int f = 0; f < 6; f++) {
+        double nw[3], dv;
+        plane_consts(w2o, kCubePt[f], kCubeN[f], nw, &dv);
+        for (int k = 0; k < 3; k++) sh[12 + f * 3 + k] = nw[k];
+      }
+    }
+  }
+  std::vector<double> mats((size_t)s.nmats * MAT, 0.0);
+  for (int m = 0; m < s.nmats; m++) {
+    const rt_material& mm = in->materials[m];
+    double* d = &mats[(size_t)m * MAT];
+    d[0] = mm.color[0];
+    d[1] = mm.color[1];
+    d[2] = mm.color[2];
+    d[3] = mm.reflectivity;
+    double fuzz = mm.fuzziness;
+    if (fuzz >= 0) {  // raytracer.go:516-522: constant offset, not random
+      double cf, sf;
+      if (!go_cos(fuzz, cf) || !go_sin(fuzz, sf)) return fail(RT_E_INVALID, "fuzziness outside restated range");
+      d[4] = fuzz * cf * cf;
+      d[5] = fuzz * sf * sf;
+      d[6] = 1.0;
+    }
+    d[7] = mm.transparency;
+    d[8] = mm.refractive_index;
+    d[9] = mm.kd;
+    d[10] = mm.ks;
+    d[11] = mm.specular_exponent;
+  }
+  std::vector<double> lights((size_t)std::max(1, s.nlights) * LGT, 0.0);
+  for (int l = 0; l < s.nlights; l++)
+    for (int k = 0; k < 3; k++) {
+      lights[(size_t)l * LGT + k] = in->lights[l].position[k];
+      lights[(size_t)l * LGT + 3 + k] = in->lights[l].color[k];
+    }
+  int rc;
+  if ((rc = upload(&s.geo, geo)) != RT_OK || (rc = upload(&s.kind, kind)) != RT_OK ||
+      (rc = upload(&s.shade, shade)) != RT_OK || (rc = upload(&s.objmat, objmat)) != RT_OK ||
+      (rc = upload(&s.mats, mats)) != RT_OK || (rc = upload(&s.lights, lights)) != RT_OK) {
+    free_scene(s);
+    return rc;
+  }
+  // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
+  int frames = std::max(1, s.depth - 1);
+  size_t need = (size_t)c->grid * frames * FRAME_FIELDS * 64 * sizeof(double);
+  if (need > c->stack_bytes) {
+    (void)hipFree(c->stack);
+    c->stack = nullptr;
+    c->stack_bytes = 0;
+    if (hipMalloc((void**)&c->stack, need) != hipSuccess) {
+      free_scene(s);
+      return fail(RT_E_NOMEM, "frame stack allocation failed");
+    }
+    c->stack_bytes = need;
+  }
+  free_scene(c->sc);
+  c->sc = s;
+  c->has_scene = true;
+  return RT_OK;
+}
+
+int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stream) {
+  if (!c || !c->has_scene) return fail(RT_E_INVALID, "rt_render_rows_async: no scene set");
+  if (!d_rgba) return fail(RT_E_INVALID, "rt_render_rows_async: NULL output");
+  const DevScene& s = c->sc;
+  if (y0 < 0 || y1 > s.height || y1 <= y0) return fail(RT_E_INVALID, "rt_render_rows_async: bad row range");
+  DeviceGuard guard(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  Params P;
+  std::memset(&P, 0, sizeof P);
+  P.geo = s.geo;
+  P.kind = s.kind;
+  P.shade = s.shade;
+  P.objmat = s.objmat;
+  P.mats = s.mats;
+  P.lights = s.lights;
+  P.jump = c->jump;
+  P.queue = c->queue;
+  P.stats = c->stats;
+  P.stack = c->stack;
+  P.out = (uint32_t*)d_rgba;
+  P.width = s.width;
+  P.height = s.height;
+  P.depth = s.depth;
+  P.nobj = s.nobj;
+  P.nlights = s.nlights;
+  P.y0 = y0;
+  P.y1 = y1;
+  P.tiles_x = (s.width + TILE - 1) / TILE;
+  int tiles_y = (y1 - y0 + TILE - 1) / TILE;
+  size_t slots = (size_t)P.tiles_x * tiles_y * TILE * TILE;
+  if (slots >= 0xFFFFFFFFull - 2u * CHUNK * (size_t)c->grid) return fail(RT_E_INVALID, "image too large for one launch");
+  P.total_slots = (unsigned int)slots;
+  P.frames = std::max(1, s.depth - 1);
+  P.vw = s.vw;
+  P.vh = s.vh;
+  for (int k = 0; k < 3; k++) {
+    P.amb[k] = s.amb[k];
+    P.bg0[k] = s.bg0[k];
+    P.bg1[k] = s.bg1[k];
+  }
+  std::memcpy(P.cube_n, c->cube_n, sizeof P.cube_n);
+  std::memcpy(P.cube_d, c->cube_d, sizeof P.cube_d);
+  HIP_TRY(hipMemsetAsync(c->queue, 0, 256, st));
+  HIP_TRY(hipEventRecord(c->ev0, st));
+  hipLaunchKernelGGL(rt_render_kernel, dim3(c->grid), dim3(64), 0, st, P);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev1, st));
+  c->timed = true;
+  c->primary_pending += (uint64_t)4 * (uint64_t)s.width * (uint64_t)(y1 - y0);
+  return RT_OK;
+}
+
+int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
+  if (!c || !out) return fail(RT_E_INVALID, "rt_read_stats: NULL argument");
+  DeviceGuard guard(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  unsigned long long h[ST_COUNT];
+  HIP_TRY(hipMemcpyAsync(h, c->stats, sizeof h, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  std::memset(out, 0, sizeof *out);
+  // Intersect calls from closestHit: every traced ray tests every object.
+  std::vector<int> kinds;
+  uint64_t per_kind[4] = {0, 0, 0, 0};
+  if (c->has_scene && c->sc.nobj > 0) {
+    kinds.resize(c->sc.nobj);
+    HIP_TRY(hipMemcpy(kinds.data(), c->sc.kind, sizeof(int) * kinds.size(), hipMemcpyDeviceToHost));
+    for (int k : kinds) per_kind[k]++;
+  }
+  out->primary_rays = c->primary_pending;
+  out->secondary_rays = h[ST_TRACED] - c->primary_pending;
+  out->shadow_rays = h[ST_SHADOW];
+  for (int k = 0; k < 4; k++) {
+    out->tests[k] = h[ST_TRACED] * per_kind[k];
+    out->shadow_tests[k] = h[ST_STESTS + k];
+  }
+  out->shaded_hits = h[ST_SHADED];
+  float ms = 0.f;
+  if (c->timed && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) out->kernel_ms = ms;
+  if (reset) {
+    HIP_TRY(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    c->primary_pending = 0;
+  }
+  return RT_OK;
+}
+
+int rt_last_kernel_ms(rt_context* c, double* ms_out) {
+  if (!c || !ms_out) return fail(RT_E_INVALID, "rt_last_kernel_ms: NULL argument");
+  if (!c->timed) return fail(RT_E_INVALID, "rt_last_kernel_ms: nothing rendered yet");
+  DeviceGuard guard(c->device);
+  HIP_TRY(hipEventSynchronize(c->ev1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  *ms_out = ms;
+  return RT_OK;
+}
+
+int rt_render(const rt_scene* scene, uint8_t* rgba_out, rt_stats* stats) {
+  if (!scene || !rgba_out) return fail(RT_E_INVALID, "rt_render: NULL argument");
+  static std::mutex mu;
+  static std::vector<rt_context*> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((int)cache.size() <= dev) cache.resize(dev + 1, nullptr);
+  if (!cache[dev]) {
+    int rc = rt_create(dev, &cache[dev]);
+    if (rc != RT_OK) return rc;
+  }
+  rt_context* c = cache[dev];
+  int rc = rt_set_scene(c, scene);
+  if (rc != RT_OK) return rc;
+  size_t bytes = (size_t)scene->width * scene->height * 4;
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, bytes));
+  rt_stats tmp;
+  rc = rt_read_stats(c, nullptr, 1, &tmp);
+  if (rc == RT_OK) rc = rt_render_rows_async(c, 0, scene->height, d, nullptr);
+  if (rc == RT_OK && hipMemcpy(rgba_out, d, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(RT_E_DEVICE, "rt_render: copy back failed");
+  if (rc == RT_OK && stats) rc = rt_read_stats(c, nullptr, 1, stats);
+  (void)hipFree(d);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,135 @@
+"""The CPU oracle against the reference's own golden vectors and KATs.
+
+Pins (reference files):
+  testdata/goldens/example_canned.png   raytracer_test.go:71-77 (canned.gml)
+  cylinder_test.go:21-165               Cylinder Intersect / normal KATs
+The reference's bar is SSIM >= 0.99 (raytracer_test.go:42); ours is exact bytes.
+"""
+import ctypes as C
+import math
+import os
+
+import numpy as np
+import pytest
+from PIL import Image
+
+import go_raytracer_amd as rt
+import oracle_bind
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load_golden(name):
+    return np.asarray(Image.open(os.path.join(GOLDEN, name)).convert("RGB"))
+
+
+def test_oracle_matches_canned_golden_exactly():
+    packed = rt.scene.convert(rt.configs.canned())
+    img, st = oracle_bind.render_rows(packed, threads=8)
+    gold = load_golden("example_canned.png")
+    assert img.shape[:2] == gold.shape[:2]
+    assert (img[..., 3] == 255).all()
+    diff = img[..., :3] != gold
+    assert int(diff.sum()) == 0, "oracle differs from example_canned.png in %d channels" % int(diff.sum())
+    assert st.primary_rays == 4 * 1900 * 1200
+
+
+def test_oracle_row_band_equals_full_frame():
+    packed = rt.scene.convert(rt.configs.canned(width=190, height=120))
+    full, _ = oracle_bind.render_rows(packed)
+    for y0, y1 in [(0, 13), (13, 47), (47, 120), (33, 34)]:
+        band, _ = oracle_bind.render_rows(packed, y0, y1)
+        assert np.array_equal(band, full[y0:y1])
+
+
+def test_oracle_thread_count_invariant():
+    packed = rt.scene.convert(rt.configs.c2(width=96, height=54))
+    a, sa = oracle_bind.render_rows(packed, threads=1)
+    b, sb = oracle_bind.render_rows(packed, threads=8)
+    assert np.array_equal(a, b)
+    assert sa.as_dict() == sb.as_dict()
+
+
+def _identity_cylinder_scene():
+    args = rt.scene.RenderArgs(ambient=(0, 0, 0), lights=[], scene=rt.scene.Cylinder(rt.scene.Material()),
+                               depth=1, fov=90.0, width=4, height=4)
+    return rt.scene.convert(args)
+
+
+def _intersect(packed, origin, direction):
+    t = C.c_double()
+    p = (C.c_double * 3)()
+    f = C.c_int()
+    ok = oracle_bind.lib().oracle_intersect(C.addressof(packed.scene), 0, (C.c_double * 3)(*origin),
+                                           (C.c_double * 3)(*direction), C.byref(t), p, C.byref(f))
+    return (ok == 1), t.value, tuple(p), f.value
+
+
+# cylinder_test.go:21-114
+@pytest.mark.parametrize("origin,direction,face,t,point", [
+    ((-2, 0.5, 0), (1, 0, 0), 0, 1.0, (-1, 0.5, 0)),     # TestCylinderIntersectSide
+    ((0, 2, 0), (0, -1, 0), 1, 1.0, None),               # TestCylinderIntersectTopCap
+    ((0, -2, 0), (0, 1, 0), 2, 2.0, None),               # TestCylinderIntersectBottomCap
+    ((0, 0.5, 0), (0, 1, 0), 1, 0.5, None),              # ...FromInsideHitsNearestCap
+])
+def test_cylinder_intersect_kats(origin, direction, face, t, point):
+    ok, tt, p, f = _intersect(_identity_cylinder_scene(), origin, direction)
+    assert ok and f == face and abs(tt - t) <= 1e-9
+    if point is not None:
+        assert math.dist(p, point) <= 1e-9
+
+
+@pytest.mark.parametrize("origin,direction", [
+    ((5, -1, 0), (0, 1, 0)), ((-2, 5, 0), (1, 0, 0)),   # TestCylinderIntersectMiss
+    ((2, 0.5, 0), (1, 0, 0)),                           # TestCylinderIntersectBehindRay
+])
+def test_cylinder_intersect_misses(origin, direction):
+    ok, _, _, _ = _intersect(_identity_cylinder_scene(), origin, direction)
+    assert not ok
+
+
+# cylinder_test.go:116-165
+@pytest.mark.parametrize("face,point,normal", [
+    (0, (1, 0.5, 0), (1, 0, 0)), (1, (0.2, 1, 0.3), (0, 1, 0)), (2, (0.2, 0, 0.3), (0, -1, 0)),
+])
+def test_cylinder_normals(face, point, normal):
+    packed = _identity_cylinder_scene()
+    nw = (C.c_double * 3)()
+    pw = (C.c_double * 3)()
+    rc = oracle_bind.lib().oracle_surface_normal(C.addressof(packed.scene), 0, face, (C.c_double * 3)(*point), nw, pw)
+    assert rc == 0 and math.dist(tuple(nw), normal) <= 1e-9
+
+
+def test_cylinder_invalid_face_is_an_error():
+    packed = _identity_cylinder_scene()
+    nw = (C.c_double * 3)()
+    pw = (C.c_double * 3)()
+    rc = oracle_bind.lib().oracle_surface_normal(C.addressof(packed.scene), 0, 99, (C.c_double * 3)(0, 0, 0), nw, pw)
+    assert rc != 0
+
+
+def test_go_pow_integer_exponents_match_repeated_squaring():
+    l = oracle_bind.lib()
+    assert l.oracle_go_pow(0.0, 50.0) == 0.0
+    assert l.oracle_go_pow(0.3, 0.0) == 1.0
+    assert l.oracle_go_pow(0.3, 1.0) == 0.3
+    assert l.oracle_go_pow(0.5, 5.0) == 0.03125
+    x = 0.987654321
+    assert abs(l.oracle_go_pow(x, 50.0) - x ** 50) <= 4e-16
+
+
+def test_go_tan_matches_libm_closely():
+    l = oracle_bind.lib()
+    for deg in (30.0, 45.0, 60.0, 89.0):
+        x = deg * math.pi / 180.0
+        assert abs(l.oracle_go_tan(x) - math.tan(x)) <= 2e-16 * max(1.0, abs(math.tan(x)))
+
+
+def test_host_gomath_sin_cos_equal_oracle():
+    from go_raytracer_amd import gomath
+    l = oracle_bind.lib()
+    rng = np.random.default_rng(3)
+    for x in rng.uniform(-20, 20, 2000):
+        x = float(x)
+        assert gomath.go_sin(x) == l.oracle_go_sin(x)
+        assert gomath.go_cos(x) == l.oracle_go_cos(x)
