@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Benchmark of the render hot path (BASELINE.json metric: Mrays/s at 4K depth 6).
+
+One step = one full frame of the workload, rows sharded across the N ranks
+(one process per GPU, RCCL gather of the bands to rank 0). N=1 workload =
+config C3 (3840x2160, depth 6, cylinder + cube + sphere-for-cone, 4 lights).
+
+Rays = primary + secondary + shadow, counted on the device with the same rule
+as the CPU oracle (include/rt_abi.h rt_stats). value = rays of all ranks per
+step / max-over-ranks step time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from __graft_entry__ import load_package  # noqa: E402
+
+# MI355X peaks (MI355X_MICROARCH.md; FP64 vector = 256 CU x 128 flop/clk x 2.4 GHz)
+PEAK_FP64_TFLOPS = 78.6
+PEAK_FP64_NOFMA_TFLOPS = 39.3  # parity build: no contraction -> one mul or add per lane-op
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", default="c3")
+    p.add_argument("--width", type=int, default=None)
+    p.add_argument("--height", type=int, default=None)
+    p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    p.add_argument("--cpu-threads", type=int, default=8)
+    return p.parse_args()
+
+
+def cpu_baseline(packed, threads):
+    """The CPU oracle (C restatement of the Go path) on this host, full frame,
+    `threads` workers over (column, 20-row) strips like raytracer.go:611-677."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind
+    t0 = time.perf_counter()
+    _, st = oracle_bind.render_rows(packed, 0, packed.height, threads=threads)
+    dt = time.perf_counter() - t0
+    rays = st.total_rays()
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": "full %dx%d frame of the same scene (%d rays, %.2f s wall)"
+                      % (packed.width, packed.height, rays, dt)}
+
+
+def main():
+    args = parse()
+    pkg = load_package()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = pkg.configs.CONFIGS[args.config]
+    kw = {}
+    if args.width:
+        kw["width"] = args.width
+    if args.height:
+        kw["height"] = args.height
+    rargs = cfg(**kw)
+    packed = pkg.scene.convert(rargs)
+    ctx = pkg.RenderContext(local)
+    ctx.set_scene(packed)
+    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        dr.step()
+    torch.cuda.synchronize()
+    ctx.read_stats(reset=True)
+
+    kernel_ms = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dr.step()
+        if dr.y1 > dr.y0:
+            kernel_ms.append(ctx.last_kernel_ms())
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    st = ctx.read_stats(reset=True)
+
+    rays_local = st.total_rays()
+    flops_local = pkg.abi.algorithmic_flops(st, len(rargs.lights))
+    kavg = sum(kernel_ms) / len(kernel_ms) if kernel_ms else 0.0
+    vals = torch.tensor([elapsed, float(rays_local), float(flops_local)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = vals.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = vals.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0].item())
+        rays_total = float(sm[1].item())
+    else:
+        rays_total = float(rays_local)
+
+    if rank == 0:
+        per_step_rays = rays_total / args.steps
+        ms_per_step = elapsed / args.steps * 1e3
+        value = rays_total / elapsed / 1e6
+        # roofline for the dominant (only) kernel: algorithmic FP64 flops per
+        # launch / average launch duration (HIP events on the launch stream)
+        flops_per_launch = flops_local / max(1, len(kernel_ms))
+        achieved_tf = flops_per_launch / (kavg * 1e-3) / 1e12 if kavg > 0 else 0.0
+        out_bytes = (dr.y1 - dr.y0) * packed.width * 4
+        line = {
+            "metric": "Mrays/s (primary+shadow+reflect) at 4K depth=6",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "%s: %s" % (args.config, (cfg.__doc__ or "").split(".")[0].strip()),
+                       "width": packed.width, "height": packed.height, "depth": rargs.depth,
+                       "lights": len(rargs.lights), "objects": int(packed.scene.num_objects),
+                       "rays_per_frame": int(per_step_rays), "parallelism": "rows%d" % world},
+            "roofline": {"bound": "valu-fp64", "achieved": round(achieved_tf, 3), "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
+                         "frac_nofma_ceiling": round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),
+                         "kernel_ms": round(kavg, 4), "flops_per_launch": int(flops_per_launch),
+                         "hbm_out_gbs": round(out_bytes / (kavg * 1e-3) / 1e9, 2) if kavg > 0 else None,
+                         "traffic": None},
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline == "auto":
+            line["cpu_baseline"] = cpu_baseline(packed, args.cpu_threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

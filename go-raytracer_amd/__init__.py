@@ -9,5 +9,5 @@ Layout:
   render.py            Render(): the reference's entry point over the C ABI
   dist.py              row-band sharding across GPUs + RCCL gather
 """
-from . import abi, configs, gomath, scene  # noqa: F401
+from . import abi, configs, dist, gomath, scene  # noqa: F401
 from .render import Render, RenderContext, load_library  # noqa: F401
