@@ -8,16 +8,26 @@
 //   raytracer.go:51-370   Sphere/Plane/Cube/Cylinder Intersect + surface props
 //   raytracer.go:724-830  scene conversion (host side, below)
 //
-// Execution model: persistent wave64 workgroups. Each LANE owns one pixel at
-// a time and runs the reference's recursion as a state machine over an
-// explicit per-lane frame stack (lane-interleaved in HBM, so pushes/pops are
-// coalesced). Waves refill idle lanes from a per-wave pool of 64 contiguous
-// pixels (one 8x8 tile) taken from a global atomic queue -- the analogue of
-// the reference's channel of (column, 20-row) work items
-// (raytracer.go:611-677) with per-lane granularity. Object loops are
-// wave-uniform (brute force over the flattened object list, exactly like
-// closestHit), so object records are fetched with scalar loads and the
-// primitive-kind switch never diverges.
+// Execution model
+//   * Persistent 256-thread workgroups = 4 independent wave64s sharing one
+//     LDS copy of the scene (staged once per workgroup; large scenes stay in
+//     HBM/L2 and are read with wave-uniform scalar loads).
+//   * Each LANE owns one pixel at a time and runs the reference's recursion
+//     as a state machine over an explicit per-lane frame stack
+//     (lane-interleaved in HBM, so pushes/pops are coalesced rows).
+//   * Lanes alternate between a TRACE pass (closestHit of the lane's current
+//     ray against every object) and a SHADE pass (surface props, lighting with
+//     shadow rays, reflection/refraction set-up). A wave only runs the SHADE
+//     pass once enough of its lanes hold a hit, so shading -- the expensive
+//     part -- runs with mostly-full lanes; lanes whose ray missed resolve
+//     their background colour and immediately trace their next ray.
+//   * Idle lanes are refilled from a per-wave pool of 64 contiguous pixels
+//     (one 8x8 tile) taken from a global atomic queue: the analogue of the
+//     reference's channel of (column, 20-row) work items
+//     (raytracer.go:611-677), with per-lane granularity.
+//   * Object loops are wave-uniform (brute force over the flattened object
+//     list, exactly like closestHit), so object records are broadcast reads
+//     and the primitive-kind switch never diverges.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -33,35 +43,39 @@
 #include "../../include/rt_abi.h"
 #include "rt_device.h"
 
+#ifndef RT_SHADE_NUM
+#define RT_SHADE_NUM 3  // shade when >= NUM/DEN of the wave's busy lanes hold a hit
+#endif
+#ifndef RT_SHADE_DEN
+#define RT_SHADE_DEN 4
+#endif
+#ifndef RT_CUBE_FAST
+#define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
+#endif
+
 using namespace rt;
 
 // ---------------------------------------------------------------------------
-// Device scene layout (built by rt_set_scene; doubles unless stated)
-// geo   [nobj][GEO]   0..11 WorldToObject rows 0-2 (prim.Mat4 affine part)
-//                     12..14 plane normal (object space), 15 plane D
-// shade [nobj][SHD]   0..11 ObjectToWorld rows 0-2, 12..29 NormalWorld per face
-// mats  [nmat][MAT]   0..2 colour, 3 reflectivity, 4..5 baked fuzz offset
+// Scene blob (built by rt_set_scene), one contiguous allocation, 16-B aligned
+// sections; strides in doubles:
+// geo    [nobj][GEO]  0..11 WorldToObject rows 0-2, 12..14 plane normal, 15 D
+// shade  [nobj][SHD]  0..11 ObjectToWorld rows 0-2, 12..29 NormalWorld per face
+// mats   [nmat][MAT]  0..2 colour, 3 reflectivity, 4..5 baked fuzz offset
 //                     (fuzz*cos^2, fuzz*sin^2; raytracer.go:517-521), 6 fuzz>=0,
 //                     7 transparency, 8 ior, 9 kd, 10 ks, 11 specular exponent
-// kind  [nobj] int32; objmat [nobj][8] int32 per-face material index
-// lights[nl][8]       0..2 position, 3..5 colour
+// lights [nl][LGT]    0..2 position, 3..5 colour
+// kind   [nobj] int32;  objmat [nobj][OMAT] int32 per-face material index
 // ---------------------------------------------------------------------------
 enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8 };
 enum { FRAME_FIELDS = 14 };  // Lw[3] cfirst[3] pend_o[3] pend_d[3] kr packed
-enum { CHUNK = 64, TILE = 8 };
-enum {
-  ST_PRIMARY = 0, ST_SECONDARY = 1, ST_SHADOW = 2, ST_TRACED = 3, ST_STESTS = 4,  // 4 kinds
-  ST_SHADED = 8, ST_COUNT = 9
-};
+enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
+enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_COUNT = 7 };
+enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
+enum { LDS_MAX_BYTES = 40 * 1024 };
 
 struct Params {
-  const double* __restrict__ geo;
-  const int* __restrict__ kind;
-  const double* __restrict__ shade;
-  const int* __restrict__ objmat;
-  const double* __restrict__ mats;
-  const double* __restrict__ lights;
-  const uint64_t* __restrict__ jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
+  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, blob_bytes;
+  const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
   unsigned int* queue;
   unsigned long long* stats;
   double* stack;
@@ -71,8 +85,6 @@ struct Params {
   int frames;  // stack frames per lane (depth - 1, >= 1)
   double vw, vh;
   double amb[3], bg0[3], bg1[3];
-  double cube_n[6][3];
-  double cube_d[6];
 };
 
 struct Ray {
@@ -81,13 +93,11 @@ struct Ray {
 
 // rayToObjectSpace (raytracer.go:51-56) with prim.Mat4.MulPoint/MulDir
 // (vec.go:298-313): m points at the 3x4 affine rows.
-__device__ __forceinline__ Ray to_obj(const double* __restrict__ m, const Ray& r) {
+__device__ __forceinline__ Ray to_obj(const double* m, const Ray& r) {
   Ray l;
-  l.o = mk(m[0] * r.o.x + m[1] * r.o.y + m[2] * r.o.z + m[3],
-           m[4] * r.o.x + m[5] * r.o.y + m[6] * r.o.z + m[7],
+  l.o = mk(m[0] * r.o.x + m[1] * r.o.y + m[2] * r.o.z + m[3], m[4] * r.o.x + m[5] * r.o.y + m[6] * r.o.z + m[7],
            m[8] * r.o.x + m[9] * r.o.y + m[10] * r.o.z + m[11]);
-  l.d = mk(m[0] * r.d.x + m[1] * r.d.y + m[2] * r.d.z,
-           m[4] * r.d.x + m[5] * r.d.y + m[6] * r.d.z,
+  l.d = mk(m[0] * r.d.x + m[1] * r.d.y + m[2] * r.d.z, m[4] * r.d.x + m[5] * r.d.y + m[6] * r.d.z,
            m[8] * r.d.x + m[9] * r.d.y + m[10] * r.d.z);
   return l;
 }
@@ -118,17 +128,50 @@ __device__ __forceinline__ bool plane_hit(const Ray& l, d3 n, double pd, double&
   return true;
 }
 
-// Cube.Intersect (raytracer.go:214-240): 6 faces; every face re-transforms the
-// ray with the same matrix in the reference, so one transform is identical.
-__device__ __forceinline__ bool cube_hit(const Params& P, const Ray& l, double& t, int& face) {
+// Cube.Intersect (raytracer.go:214-240) over prim.PlanesForUnitCube
+// (internal/prim/plane.go:29-38). Every face re-transforms the ray with the
+// same matrix in the reference, so one transform gives identical values.
+// With RT_CUBE_FAST the face planes' dot products are evaluated on the one
+// non-zero axis: for a finite ray, n.v = (0*a + 0*b) + (+-1)*c equals +-c
+// exactly whenever c != 0, and when c == 0 both forms are a zero that is
+// rejected identically (|denom| < 1e-6, or t = 0 <= 0), so hits, T and
+// PointObj are bit-identical to the generic dot products.
+__device__ __forceinline__ bool cube_face(const Ray& l, int f, double& best, int& bf, bool& found) {
+  // face f: axis, sign of the normal, -D (D = -normal.Dot(point))
+  const int ax = (f < 2) ? 2 : ((f < 4) ? 0 : 1);
+  const bool pos = (f == 1 || f == 3 || f == 4);
+  const double negD = (f == 1 || f == 3 || f == 4) ? 1.0 : 0.0;
+  double dA = ax == 0 ? l.d.x : (ax == 1 ? l.d.y : l.d.z);
+  double oA = ax == 0 ? l.o.x : (ax == 1 ? l.o.y : l.o.z);
+  double denom = pos ? dA : -dA;
+  if (__builtin_fabs(denom) < 1e-6) return false;
+  double nO = pos ? oA : -oA;
+  double tt = (negD - nO) / denom;
+  if (tt <= 0.0) return false;
+  d3 p = add(l.o, scale(l.d, tt));
+  if (p.x < 0 || p.x > 1 || p.y < 0 || p.y > 1 || p.z < 0 || p.z > 1) return false;
+  if (!found || tt < best) {
+    found = true;
+    best = tt;
+    bf = f;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool cube_hit(const Ray& l, double& t, int& face) {
   bool found = false;
   double best = 0.0;
   int bf = 0;
+#if RT_CUBE_FAST
+#pragma unroll
+  for (int f = 0; f < 6; f++) cube_face(l, f, best, bf, found);
+#else
+  const double N[6][3] = {{0, 0, -1}, {0, 0, 1}, {-1, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, -1, 0}};
+  const double D[6] = {-0.0, -1.0, -0.0, -1.0, -1.0, -0.0};
 #pragma unroll
   for (int f = 0; f < 6; f++) {
     double ft;
-    d3 n = mk(P.cube_n[f][0], P.cube_n[f][1], P.cube_n[f][2]);
-    if (!plane_hit(l, n, P.cube_d[f], ft)) continue;
+    if (!plane_hit(l, mk(N[f][0], N[f][1], N[f][2]), D[f], ft)) continue;
     if (ft < 0.0) continue;
     d3 p = add(l.o, scale(l.d, ft));
     if (p.x < 0 || p.x > 1 || p.y < 0 || p.y > 1 || p.z < 0 || p.z > 1) continue;
@@ -138,6 +181,7 @@ __device__ __forceinline__ bool cube_hit(const Params& P, const Ray& l, double& 
       bf = f;
     }
   }
+#endif
   if (found) {
     t = best;
     face = bf;
@@ -191,9 +235,8 @@ __device__ __forceinline__ bool cylinder_hit(const Ray& l, double& t, int& face)
   return true;
 }
 
-// One SceneObject.Intersect on a world-space ray; kind is wave-uniform.
-__device__ __forceinline__ bool object_hit(const Params& P, int k, const double* __restrict__ g, const Ray& r,
-                                           double& t, int& face) {
+// One SceneObject.Intersect on a world-space ray; k is wave-uniform.
+__device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r, double& t, int& face) {
   Ray l = to_obj(g, r);
   face = 0;
   switch (k) {
@@ -202,7 +245,7 @@ __device__ __forceinline__ bool object_hit(const Params& P, int k, const double*
     case RT_PLANE:
       return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
     case RT_CUBE:
-      return cube_hit(P, l, t, face);
+      return cube_hit(l, t, face);
     default:
       return cylinder_hit(l, t, face);
   }
@@ -231,14 +274,47 @@ __device__ __forceinline__ d3 combine(bool tmode, d3 lw, d3 col, double refl, do
   return clamp(mul(add(lw, add(scale(R, kr), scale(Tr, 1.0 - kr))), col));
 }
 
-__global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
-  const int lane = (int)__lane_id();
-  double* stk = P.stack + (size_t)blockIdx.x * ((size_t)P.frames * FRAME_FIELDS * 64) + lane;
+struct View {
+  const double* geo;
+  const double* shade;
+  const double* mats;
+  const double* lights;
+  const int* kind;
+  const int* objmat;
+};
+
+template <bool LDS>
+__global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ blob, Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const char* base;
+  if constexpr (LDS) {
+    // Stage the whole scene once per workgroup (the only block-wide barrier).
+    const int n16 = P.blob_bytes / 16;
+    for (int i = threadIdx.x; i < n16; i += WG)
+      reinterpret_cast<uint4*>(smem)[i] = reinterpret_cast<const uint4*>(blob)[i];
+    __syncthreads();
+    base = smem;
+  } else {
+    base = blob;
+  }
+  View S;
+  S.geo = reinterpret_cast<const double*>(base + P.off_geo);
+  S.shade = reinterpret_cast<const double*>(base + P.off_shade);
+  S.mats = reinterpret_cast<const double*>(base + P.off_mats);
+  S.lights = reinterpret_cast<const double*>(base + P.off_lights);
+  S.kind = reinterpret_cast<const int*>(base + P.off_kind);
+  S.objmat = reinterpret_cast<const int*>(base + P.off_objmat);
+
+  const int lane = (int)(threadIdx.x & 63);
+  const int wslot = (int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
+  double* stk = P.stack + (size_t)wslot * ((size_t)P.frames * FRAME_FIELDS * 64) + lane;
   const d3 eye = mk(0.0, 0.0, -1.0);  // raytracer.go:605-609
 
   // lane state
-  bool alive = false;
+  int state = S_IDLE;
   int px = 0, py = 0, sample = 0, sp = 0;
+  int hit_i = 0, hit_f = 0;
+  double hit_t = 0.0;
   Pcg rng{0, 0};
   d3 sum = mk(0, 0, 0);
   Ray ray;
@@ -248,7 +324,7 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
   // wave-uniform pool and counters
   unsigned int pool_next = 0, pool_end = 0;
   bool exhausted = false;
-  uint64_t c_primary = 0, c_secondary = 0, c_shadow = 0, c_traced = 0, c_shaded = 0;
+  uint64_t c_shadow = 0, c_traced = 0, c_shaded = 0;
   uint64_t c_stest[4] = {0, 0, 0, 0};
 
   const double W1 = (double)(P.width - 1), H1 = (double)(P.height - 1);
@@ -263,26 +339,79 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
     ray.d = norm(sub(ray.o, eye));
   };
 
+  // Propagate a finished traceRay colour up the lane's frame stack
+  // (post-order, raytracer.go:528/554/557-561); ends with the lane either
+  // tracing its next ray (pending refraction child / next sample) or idle.
+  auto unwind = [&](bool have_res, d3 res) {
+    while (__any(have_res)) {
+      if (have_res) {
+        if (sp == 0) {
+          sum = add(sum, res);  // raytracer.go:651
+          sample++;
+          if (sample == 4) {
+            d3 c = scale(sum, 1.0 / 4.0);  // raytracer.go:656 -> vec.go:104-107
+            uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
+            uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
+            uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
+            P.out[(size_t)(py - P.y0) * (size_t)P.width + (size_t)px] =
+                (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+            state = S_IDLE;
+          } else {
+            gen_ray();
+            state = S_TRACE;
+          }
+          have_res = false;
+        } else {
+          double* f = frame_ptr(stk, sp - 1);
+          long long packed = __double_as_longlong(f[13 * 64]);
+          int fl = (int)(packed & 0xff);
+          if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
+            // reflection child done; trace the pending refraction child
+            st3(f, 3, res);
+            f[13 * 64] = __longlong_as_double(packed | FL_STAGE);
+            ray.o = ld3(f, 6);
+            ray.d = ld3(f, 9);
+            state = S_TRACE;
+            have_res = false;
+          } else {
+            const double* FM = S.mats + (size_t)(packed >> 8) * MAT;
+            d3 R = mk(0, 0, 0), Tr = mk(0, 0, 0);
+            if ((fl & FL_HASR) && (fl & FL_HAST)) {
+              R = ld3(f, 3);
+              Tr = res;
+            } else if (fl & FL_HASR) {
+              R = res;
+            } else {
+              Tr = res;
+            }
+            res = combine((fl & FL_TMODE) != 0, ld3(f, 0), mk(FM[0], FM[1], FM[2]), FM[3], f[12 * 64], R, Tr);
+            sp--;
+          }
+        }
+      }
+    }
+  };
+
   for (;;) {
     // ---- refill idle lanes from the wave pool (one 8x8 tile per chunk) ----
     for (;;) {
-      bool need = !alive;
+      bool need = state == S_IDLE;
       uint64_t mask = __ballot(need);
       if (mask == 0 || exhausted) break;
       if (pool_next >= pool_end) {
-        unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(P.queue, (unsigned int)CHUNK);
-        base = __shfl(base, 0);
-        if (base >= P.total_slots) {
+        unsigned int b = 0;
+        if (lane == 0) b = atomicAdd(P.queue, (unsigned int)CHUNK);
+        b = __shfl(b, 0);
+        if (b >= P.total_slots) {
           exhausted = true;
           break;
         }
-        pool_next = base;
-        pool_end = min(base + (unsigned int)CHUNK, P.total_slots);
+        pool_next = b;
+        pool_end = min(b + (unsigned int)CHUNK, P.total_slots);
       }
-      unsigned int rank = __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
-      unsigned int navail = pool_end - pool_next;
-      unsigned int take = min((unsigned int)__popcll(mask), navail);
+      unsigned int rank = __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
+      unsigned int take = min((unsigned int)__popcll(mask), pool_end - pool_next);
       if (need && rank < take) {
         unsigned int slot = pool_next + rank;
         unsigned int tile = slot / (TILE * TILE), within = slot % (TILE * TILE);
@@ -301,103 +430,113 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
           sum = mk(0, 0, 0);
           sp = 0;
           gen_ray();
-          alive = true;
+          state = S_TRACE;
         }
       }
       pool_next += take;
     }
-    if (!__any(alive)) break;
-    c_primary += 0;  // primaries are counted when generated (below)
+    if (!__any(state != S_IDLE)) break;
 
-    // ---- closestHit over all objects (raytracer.go:469-483) ----
-    bool found = false;
-    double best_t = 0.0;
-    int best_i = 0, best_f = 0;
-    for (int i = 0; i < P.nobj; i++) {
-      const int k = P.kind[i];
-      const double* g = P.geo + (size_t)i * GEO;
-      if (alive) {
-        double t;
-        int f;
-        if (object_hit(P, k, g, ray, t, f)) {
-          if (!found || t < best_t) {
-            found = true;
-            best_t = t;
-            best_i = i;
-            best_f = f;
+    // ---- TRACE pass: closestHit over all objects (raytracer.go:469-483) ----
+    if (__any(state == S_TRACE)) {
+      const bool tr = state == S_TRACE;
+      bool found = false;
+      double best_t = 0.0;
+      int best_i = 0, best_f = 0;
+      for (int i = 0; i < P.nobj; i++) {
+        const int k = S.kind[i];
+        const double* g = S.geo + (size_t)i * GEO;
+        if (tr) {
+          double t;
+          int f;
+          if (object_hit(k, g, ray, t, f)) {
+            if (!found || t < best_t) {
+              found = true;
+              best_t = t;
+              best_i = i;
+              best_f = f;
+            }
           }
         }
       }
+      c_traced += popc_ballot(tr);
+      d3 res = mk(0, 0, 0);
+      if (tr) {
+        if (found) {
+          state = S_SHADE;
+          hit_i = best_i;
+          hit_f = best_f;
+          hit_t = best_t;
+        } else {  // background gradient, raytracer.go:493-497
+          double t = 0.5 * (ray.d.y + 1.0);
+          res = lerp(mk(P.bg0[0], P.bg0[1], P.bg0[2]), mk(P.bg1[0], P.bg1[1], P.bg1[2]), t);
+        }
+      }
+      unwind(tr && !found, res);
     }
-    c_traced += popc_ballot(alive);
 
-    bool have_res = false;
-    d3 res = mk(0, 0, 0);
-    if (alive && !found) {  // background gradient, raytracer.go:493-497
-      double t = 0.5 * (ray.d.y + 1.0);
-      res = lerp(mk(P.bg0[0], P.bg0[1], P.bg0[2]), mk(P.bg1[0], P.bg1[1], P.bg1[2]), t);
-      have_res = true;
-    }
-    const bool hit = alive && found;
-    c_shaded += popc_ballot(hit);
+    // ---- SHADE pass, once enough lanes hold a hit ----
+    const uint64_t nsh = popc_ballot(state == S_SHADE);
+    const uint64_t ntr = popc_ballot(state == S_TRACE);
+    if (nsh == 0 || (ntr != 0 && nsh * RT_SHADE_DEN < (nsh + ntr) * RT_SHADE_NUM)) continue;
 
-    // ---- ComputeSurfaceProps (raytracer.go:106-122, 182-194, 242-260, 339-370) ----
+    const bool hit = state == S_SHADE;
+    c_shaded += nsh;
+    // ComputeSurfaceProps (raytracer.go:106-122, 182-194, 242-260, 339-370)
     d3 pw = mk(0, 0, 0), nw = mk(0, 0, 1);
     int mat = 0;
     if (hit) {
-      const double* g = P.geo + (size_t)best_i * GEO;
-      const double* s = P.shade + (size_t)best_i * SHD;
-      const int k = P.kind[best_i];
+      const double* g = S.geo + (size_t)hit_i * GEO;
+      const double* s = S.shade + (size_t)hit_i * SHD;
+      const int k = S.kind[hit_i];
       Ray l = to_obj(g, ray);
-      d3 p = add(l.o, scale(l.d, best_t));  // Hit.PointObj
+      d3 p = add(l.o, scale(l.d, hit_t));  // Hit.PointObj
       pw = mk(s[0] * p.x + s[1] * p.y + s[2] * p.z + s[3], s[4] * p.x + s[5] * p.y + s[6] * p.z + s[7],
               s[8] * p.x + s[9] * p.y + s[10] * p.z + s[11]);
       if (k == RT_SPHERE) {
         nw = p;
       } else if (k == RT_CYLINDER) {
-        d3 n = best_f == 0 ? mk(p.x, 0, p.z) : (best_f == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
+        d3 n = hit_f == 0 ? mk(p.x, 0, p.z) : (hit_f == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
         // NormalMat = WorldToObject^T (raytracer.go:814): MulDir then Normalize.
         nw = norm(mk(g[0] * n.x + g[4] * n.y + g[8] * n.z, g[1] * n.x + g[5] * n.y + g[9] * n.z,
                      g[2] * n.x + g[6] * n.y + g[10] * n.z));
       } else {
-        nw = mk(s[12 + best_f * 3], s[13 + best_f * 3], s[14 + best_f * 3]);
+        nw = mk(s[12 + hit_f * 3], s[13 + hit_f * 3], s[14 + hit_f * 3]);
       }
-      mat = P.objmat[(size_t)best_i * OMAT + best_f];
+      mat = S.objmat[(size_t)hit_i * OMAT + hit_f];
     }
 
-    // ---- computeLighting + inShadow (raytracer.go:372-429) ----
+    // computeLighting + inShadow (raytracer.go:372-429)
+    const double* M = S.mats + (size_t)mat * MAT;
     d3 L = mk(0, 0, 0);
-    const double* M = P.mats + (size_t)mat * MAT;
     if (hit) L = scale(mk(P.amb[0], P.amb[1], P.amb[2]), M[9]);
     const double rlen = len(ray.d);
     const d3 sorig = add(pw, scale(nw, 1e-4));
     for (int li = 0; li < P.nlights; li++) {
-      const double* lt = P.lights + (size_t)li * LGT;
-      d3 lpos = mk(lt[0], lt[1], lt[2]);
-      d3 lth = sub(lpos, pw);
+      const double* lt = S.lights + (size_t)li * LGT;
+      d3 lth = sub(mk(lt[0], lt[1], lt[2]), pw);
       double dist = len(lth);
       d3 ldir = norm(lth);
-      c_shadow += popc_ballot(hit);
+      c_shadow += nsh;
       bool open = hit;  // lanes still looking for an occluder
       Ray sr;
       sr.o = sorig;
       sr.d = ldir;
       for (int i = 0; i < P.nobj; i++) {
         if (!__any(open)) break;
-        const int k = P.kind[i];
-        const double* g = P.geo + (size_t)i * GEO;
-        bool test = open && i != best_i;
+        const int k = S.kind[i];
+        const double* g = S.geo + (size_t)i * GEO;
+        bool test = open && i != hit_i;
         c_stest[k] += popc_ballot(test);
         if (test) {
           double t;
           int f;
-          if (object_hit(P, k, g, sr, t, f)) {
+          if (object_hit(k, g, sr, t, f)) {
             if (t * rlen < dist) open = false;
           }
         }
       }
-      bool lit = hit && open;
-      if (lit) {
+      if (hit && open) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
         double ndl = go_max(0, dot(nw, ldir));
         d3 diffuse = scale(lcol, ndl * M[9]);
@@ -408,7 +547,9 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
       }
     }
 
-    // ---- traceRay body after lighting (raytracer.go:505-561) ----
+    // traceRay body after lighting (raytracer.go:505-561)
+    bool have_res = false;
+    d3 res = mk(0, 0, 0);
     if (hit) {
       d3 col = mk(M[0], M[1], M[2]);
       double refl = M[3], T = M[7];
@@ -428,9 +569,9 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
         }
         bool tmode = T > 0;
         bool hasT = false;
-        Ray tr;
-        tr.o = mk(0, 0, 0);
-        tr.d = mk(0, 0, 1);
+        Ray trr;
+        trr.o = mk(0, 0, 0);
+        trr.d = mk(0, 0, 1);
         double kr = 0.0;
         d3 lw = L;
         if (tmode) {
@@ -450,8 +591,8 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
             d3 td = add(scale(ray.d, ratio), scale(nn, ratio * cosI - cosT));
             if (!iszero(td)) {
               hasT = true;
-              tr.o = sub(pw, scale(nn, 1e-4));
-              tr.d = td;
+              trr.o = sub(pw, scale(nn, 1e-4));
+              trr.d = td;
             }
           }
           // fresnel (raytracer.go:456-467) on the unflipped normal
@@ -467,75 +608,25 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
           double* f = frame_ptr(stk, sp);
           st3(f, 0, lw);
           if (hasR && hasT) {
-            st3(f, 6, tr.o);
-            st3(f, 9, tr.d);
+            st3(f, 6, trr.o);
+            st3(f, 9, trr.d);
           }
           f[12 * 64] = kr;
-          long long packed = ((long long)mat << 8) | (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
+          long long packed =
+              ((long long)mat << 8) | (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
           f[13 * 64] = __longlong_as_double(packed);
           sp++;
-          ray = hasR ? rr : tr;
+          ray = hasR ? rr : trr;
+          state = S_TRACE;
         } else {
           res = combine(tmode, lw, col, refl, kr, mk(0, 0, 0), mk(0, 0, 0));
           have_res = true;
         }
       }
     }
-    // lanes that pushed a frame trace a secondary ray next iteration
-    c_secondary += popc_ballot(hit && !have_res);
-
-    // ---- unwind: propagate results up the frame stack (post-order) ----
-    while (__any(have_res)) {
-      if (have_res) {
-        if (sp == 0) {
-          sum = add(sum, res);  // raytracer.go:651
-          sample++;
-          if (sample == 4) {
-            d3 c = scale(sum, 1.0 / 4.0);  // raytracer.go:656 -> vec.go:104-107
-            uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
-            uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
-            uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
-            P.out[(size_t)(py - P.y0) * (size_t)P.width + (size_t)px] =
-                (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
-            alive = false;
-          } else {
-            gen_ray();
-          }
-          have_res = false;
-        } else {
-          double* f = frame_ptr(stk, sp - 1);
-          long long packed = __double_as_longlong(f[13 * 64]);
-          int fl = (int)(packed & 0xff);
-          int fm = (int)(packed >> 8);
-          if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
-            // reflection child done; trace the pending refraction child
-            st3(f, 3, res);
-            f[13 * 64] = __longlong_as_double(packed | FL_STAGE);
-            ray.o = ld3(f, 6);
-            ray.d = ld3(f, 9);
-            have_res = false;
-          } else {
-            const double* FM = P.mats + (size_t)fm * MAT;
-            d3 R = mk(0, 0, 0), Tr = mk(0, 0, 0);
-            if ((fl & FL_HASR) && (fl & FL_HAST)) {
-              R = ld3(f, 3);
-              Tr = res;
-            } else if (fl & FL_HASR) {
-              R = res;
-            } else {
-              Tr = res;
-            }
-            res = combine((fl & FL_TMODE) != 0, ld3(f, 0), mk(FM[0], FM[1], FM[2]), FM[3], f[12 * 64], R, Tr);
-            sp--;
-          }
-        }
-      }
-    }
-    c_secondary += 0;
-    // count lanes that started a pending refraction child or a new sample
+    unwind(have_res, res);
   }
 
-  // primaries are exactly 4 per pixel; secondaries = traced - primaries
   if (lane == 0) {
     atomicAdd(P.stats + ST_TRACED, (unsigned long long)c_traced);
     atomicAdd(P.stats + ST_SHADOW, (unsigned long long)c_shadow);
@@ -544,6 +635,8 @@ __global__ __launch_bounds__(64) void rt_render_kernel(Params P) {
   }
 }
 
+template __global__ void rt_render_kernel<true>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<false>(const char* __restrict__, Params);
 // ===========================================================================
 // Host side: scene conversion (raytracer.go:724-830) and the C ABI
 // ===========================================================================
@@ -697,20 +790,20 @@ struct DevScene {
   int width = 0, height = 0, depth = 0, nobj = 0, nlights = 0, nmats = 0;
   double vw = 0, vh = 0;
   double amb[3] = {0, 0, 0}, bg0[3] = {0, 0, 0}, bg1[3] = {0, 0, 0};
-  double* geo = nullptr;
-  int* kind = nullptr;
-  double* shade = nullptr;
-  int* objmat = nullptr;
-  double* mats = nullptr;
-  double* lights = nullptr;
+  char* blob = nullptr;
+  int blob_bytes = 0;
+  int off_geo = 0, off_shade = 0, off_mats = 0, off_lights = 0, off_kind = 0, off_objmat = 0;
+  std::vector<int> kinds;  // host copy for the per-kind test counts
 };
+
+int align16(int v) { return (v + 15) & ~15; }
 
 }  // namespace
 
 struct rt_context {
   int device = 0;
   int cus = 0;
-  int grid = 0;
+  int grid_lds = 0, grid_glb = 0;  // persistent grids (workgroups) per kernel flavour
   DevScene sc;
   bool has_scene = false;
   uint64_t* jump = nullptr;
@@ -721,8 +814,6 @@ struct rt_context {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   uint64_t primary_pending = 0;  // host-side count of launched primary rays
-  double cube_n[6][3];
-  double cube_d[6];
 };
 
 namespace {
@@ -739,12 +830,7 @@ struct DeviceGuard {
 };
 
 void free_scene(DevScene& s) {
-  (void)hipFree(s.geo);
-  (void)hipFree(s.kind);
-  (void)hipFree(s.shade);
-  (void)hipFree(s.objmat);
-  (void)hipFree(s.mats);
-  (void)hipFree(s.lights);
+  (void)hipFree(s.blob);
   s = DevScene();
 }
 
@@ -780,10 +866,18 @@ int rt_create(int device, rt_context** out) {
     return fail(RT_E_DEVICE, "hipGetDeviceProperties failed");
   }
   c->cus = prop.multiProcessorCount;
+  // Persistent grids: as many workgroups as are resident (any extra block just
+  // finds the queue drained). The LDS flavour is sized for the LDS budget.
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel, 64, 0) != hipSuccess || per_cu <= 0)
-    per_cu = 8;
-  c->grid = c->cus * std::min(per_cu, 32);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, WG, LDS_MAX_BYTES) !=
+          hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  c->grid_lds = c->cus * std::min(per_cu, 8);
+  per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false>, WG, 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 2;
+  c->grid_glb = c->cus * std::min(per_cu, 8);
   // PCG jump table: 8*r LCG steps, r = 0..19 (pcg.go: mul/inc constants).
   std::vector<uint64_t> jump(20 * 4);
   {
@@ -811,11 +905,6 @@ int rt_create(int device, rt_context** out) {
     rc = fail(RT_E_DEVICE, "stats memset");
   if (rc == RT_OK && (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess))
     rc = fail(RT_E_DEVICE, "event create");
-  // Cube face planes: normal and D = -normal.Dot(point), same op order as Go.
-  for (int f = 0; f < 6; f++) {
-    for (int k = 0; k < 3; k++) c->cube_n[f][k] = kCubeN[f][k];
-    c->cube_d[f] = -(kCubeN[f][0] * kCubePt[f][0] + kCubeN[f][1] * kCubePt[f][1] + kCubeN[f][2] * kCubePt[f][2]);
-  }
   if (rc != RT_OK) {
     rt_destroy(c);
     return rc;
@@ -931,16 +1020,32 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       lights[(size_t)l * LGT + k] = in->lights[l].position[k];
       lights[(size_t)l * LGT + 3 + k] = in->lights[l].color[k];
     }
-  int rc;
-  if ((rc = upload(&s.geo, geo)) != RT_OK || (rc = upload(&s.kind, kind)) != RT_OK ||
-      (rc = upload(&s.shade, shade)) != RT_OK || (rc = upload(&s.objmat, objmat)) != RT_OK ||
-      (rc = upload(&s.mats, mats)) != RT_OK || (rc = upload(&s.lights, lights)) != RT_OK) {
-    free_scene(s);
-    return rc;
+  // One blob: geo | shade | mats | lights | kind | objmat (16-B aligned sections).
+  s.off_geo = 0;
+  s.off_shade = align16(s.off_geo + (int)(geo.size() * sizeof(double)));
+  s.off_mats = align16(s.off_shade + (int)(shade.size() * sizeof(double)));
+  s.off_lights = align16(s.off_mats + (int)(mats.size() * sizeof(double)));
+  s.off_kind = align16(s.off_lights + (int)(lights.size() * sizeof(double)));
+  s.off_objmat = align16(s.off_kind + (int)(kind.size() * sizeof(int)));
+  s.blob_bytes = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
+  {
+    std::vector<char> blob((size_t)s.blob_bytes, 0);
+    std::memcpy(blob.data() + s.off_geo, geo.data(), geo.size() * sizeof(double));
+    std::memcpy(blob.data() + s.off_shade, shade.data(), shade.size() * sizeof(double));
+    std::memcpy(blob.data() + s.off_mats, mats.data(), mats.size() * sizeof(double));
+    std::memcpy(blob.data() + s.off_lights, lights.data(), lights.size() * sizeof(double));
+    std::memcpy(blob.data() + s.off_kind, kind.data(), kind.size() * sizeof(int));
+    std::memcpy(blob.data() + s.off_objmat, objmat.data(), objmat.size() * sizeof(int));
+    int rc = upload(&s.blob, blob);
+    if (rc != RT_OK) {
+      free_scene(s);
+      return rc;
+    }
   }
+  s.kinds = kind;
   // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
   int frames = std::max(1, s.depth - 1);
-  size_t need = (size_t)c->grid * frames * FRAME_FIELDS * 64 * sizeof(double);
+  size_t need = (size_t)std::max(c->grid_lds, c->grid_glb) * WAVES_PER_WG * frames * FRAME_FIELDS * 64 * sizeof(double);
   if (need > c->stack_bytes) {
     (void)hipFree(c->stack);
     c->stack = nullptr;
@@ -964,14 +1069,17 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
   if (y0 < 0 || y1 > s.height || y1 <= y0) return fail(RT_E_INVALID, "rt_render_rows_async: bad row range");
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
+  const bool lds = s.blob_bytes <= LDS_MAX_BYTES;
+  const int grid = lds ? c->grid_lds : c->grid_glb;
   Params P;
   std::memset(&P, 0, sizeof P);
-  P.geo = s.geo;
-  P.kind = s.kind;
-  P.shade = s.shade;
-  P.objmat = s.objmat;
-  P.mats = s.mats;
-  P.lights = s.lights;
+  P.off_geo = s.off_geo;
+  P.off_shade = s.off_shade;
+  P.off_mats = s.off_mats;
+  P.off_lights = s.off_lights;
+  P.off_kind = s.off_kind;
+  P.off_objmat = s.off_objmat;
+  P.blob_bytes = s.blob_bytes;
   P.jump = c->jump;
   P.queue = c->queue;
   P.stats = c->stats;
@@ -987,7 +1095,8 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
   P.tiles_x = (s.width + TILE - 1) / TILE;
   int tiles_y = (y1 - y0 + TILE - 1) / TILE;
   size_t slots = (size_t)P.tiles_x * tiles_y * TILE * TILE;
-  if (slots >= 0xFFFFFFFFull - 2u * CHUNK * (size_t)c->grid) return fail(RT_E_INVALID, "image too large for one launch");
+  if (slots >= 0xFFFFFFFFull - 2u * CHUNK * (size_t)grid * WAVES_PER_WG)
+    return fail(RT_E_INVALID, "image too large for one launch");
   P.total_slots = (unsigned int)slots;
   P.frames = std::max(1, s.depth - 1);
   P.vw = s.vw;
@@ -997,11 +1106,12 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
     P.bg0[k] = s.bg0[k];
     P.bg1[k] = s.bg1[k];
   }
-  std::memcpy(P.cube_n, c->cube_n, sizeof P.cube_n);
-  std::memcpy(P.cube_d, c->cube_d, sizeof P.cube_d);
   HIP_TRY(hipMemsetAsync(c->queue, 0, 256, st));
   HIP_TRY(hipEventRecord(c->ev0, st));
-  hipLaunchKernelGGL(rt_render_kernel, dim3(c->grid), dim3(64), 0, st, P);
+  if (lds)
+    hipLaunchKernelGGL(rt_render_kernel<true>, dim3(grid), dim3(WG), s.blob_bytes, st, (const char*)s.blob, P);
+  else
+    hipLaunchKernelGGL(rt_render_kernel<false>, dim3(grid), dim3(WG), 0, st, (const char*)s.blob, P);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   c->timed = true;
@@ -1018,13 +1128,9 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
   HIP_TRY(hipStreamSynchronize(st));
   std::memset(out, 0, sizeof *out);
   // Intersect calls from closestHit: every traced ray tests every object.
-  std::vector<int> kinds;
   uint64_t per_kind[4] = {0, 0, 0, 0};
-  if (c->has_scene && c->sc.nobj > 0) {
-    kinds.resize(c->sc.nobj);
-    HIP_TRY(hipMemcpy(kinds.data(), c->sc.kind, sizeof(int) * kinds.size(), hipMemcpyDeviceToHost));
-    for (int k : kinds) per_kind[k]++;
-  }
+  if (c->has_scene)
+    for (int k : c->sc.kinds) per_kind[k]++;
   out->primary_rays = c->primary_pending;
   out->secondary_rays = h[ST_TRACED] - c->primary_pending;
   out->shadow_rays = h[ST_SHADOW];
