@@ -49,6 +49,15 @@
 #ifndef RT_SHADE_DEN
 #define RT_SHADE_DEN 4
 #endif
+#ifndef RT_DIV_SKIP
+#define RT_DIV_SKIP 1  // skip divisions whose sign already proves t <= 0 (exact, see t_nonpos)
+#endif
+#ifndef RT_FRAME_PREFETCH
+#define RT_FRAME_PREFETCH 1  // load the parent frame during the TRACE pass
+#endif
+#ifndef RT_CULL
+#define RT_CULL 1  // wave-uniform conservative bounding-sphere culling (exact, see may_hit)
+#endif
 #ifndef RT_CUBE_FAST
 #define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
 #endif
@@ -58,7 +67,9 @@ using namespace rt;
 // ---------------------------------------------------------------------------
 // Scene blob (built by rt_set_scene), one contiguous allocation, 16-B aligned
 // sections; strides in doubles:
-// geo    [nobj][GEO]  0..11 WorldToObject rows 0-2, 12..14 plane normal, 15 D
+// geo    [nobj][GEO]  0..11 WorldToObject rows 0-2; planes: 12..14 normal, 15 D;
+//                     bounded kinds: 12..13 = 4 floats (centre xyz, padded
+//                     radius^2) of a world-space bounding sphere (culling only)
 // shade  [nobj][SHD]  0..11 ObjectToWorld rows 0-2, 12..29 NormalWorld per face
 // mats   [nmat][MAT]  0..2 colour, 3 reflectivity, 4..5 baked fuzz offset
 //                     (fuzz*cos^2, fuzz*sin^2; raytracer.go:517-521), 6 fuzz>=0,
@@ -69,9 +80,12 @@ using namespace rt;
 enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8 };
 enum { FRAME_FIELDS = 14 };  // Lw[3] cfirst[3] pend_o[3] pend_d[3] kr packed
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
-enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_COUNT = 7 };
+enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_COUNT = 7, ST_PHASE = 16, N_PHASE = 8 };
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
-enum { LDS_MAX_BYTES = 40 * 1024 };
+#ifndef RT_LDS_MAX
+#define RT_LDS_MAX (40 * 1024)
+#endif
+enum { LDS_MAX_BYTES = RT_LDS_MAX };
 
 struct Params {
   int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, blob_bytes;
@@ -102,6 +116,18 @@ __device__ __forceinline__ Ray to_obj(const double* m, const Ray& r) {
   return l;
 }
 
+// True when q = num/den (den != 0, finite) is certainly <= 0, i.e. num == 0
+// or the signs differ, so the reference would reject t = q (t <= 0) and the
+// division can be skipped. NaN operands return false (the division runs and
+// the NaN flows through exactly as in the reference).
+__device__ __forceinline__ bool t_nonpos(double num, double den) {
+#if RT_DIV_SKIP
+  return (num == 0.0 && !__builtin_isnan(den)) || (num < 0.0 && den > 0.0) || (num > 0.0 && den < 0.0);
+#else
+  return false;
+#endif
+}
+
 // Sphere.Intersect (raytracer.go:58-104): unit sphere, near root only.
 __device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
   double a = dot(l.d, l.d);
@@ -110,7 +136,9 @@ __device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
   double disc = hb * hb - a * c;
   if (disc < 0.0) return false;
   double sq = __builtin_sqrt(disc);
-  double t0 = (-hb - sq) / a;
+  double num = -hb - sq;
+  if (t_nonpos(num, a)) return false;  // t0 <= 0: no near hit
+  double t0 = num / a;
   if (t0 > 0.0) {
     t = t0;
     return true;
@@ -122,7 +150,9 @@ __device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
 __device__ __forceinline__ bool plane_hit(const Ray& l, d3 n, double pd, double& t) {
   double denom = dot(n, l.d);
   if (__builtin_fabs(denom) < 1e-6) return false;
-  double tt = (-pd - dot(n, l.o)) / denom;
+  double num = -pd - dot(n, l.o);
+  if (t_nonpos(num, denom)) return false;
+  double tt = num / denom;
   if (tt <= 0.0) return false;
   t = tt;
   return true;
@@ -146,7 +176,9 @@ __device__ __forceinline__ bool cube_face(const Ray& l, int f, double& best, int
   double denom = pos ? dA : -dA;
   if (__builtin_fabs(denom) < 1e-6) return false;
   double nO = pos ? oA : -oA;
-  double tt = (negD - nO) / denom;
+  double num = negD - nO;
+  if (t_nonpos(num, denom)) return false;
+  double tt = num / denom;
   if (tt <= 0.0) return false;
   d3 p = add(l.o, scale(l.d, tt));
   if (p.x < 0 || p.x > 1 || p.y < 0 || p.y > 1 || p.z < 0 || p.z > 1) return false;
@@ -200,33 +232,45 @@ __device__ __forceinline__ bool cylinder_hit(const Ray& l, double& t, int& face)
     double disc = hb * hb - a * c0;
     if (disc >= 0.0) {
       double sq = __builtin_sqrt(disc);
-      double t0 = (-hb - sq) / a;
-      double t1 = (-hb + sq) / a;
-      double y0 = l.o.y + l.d.y * t0;
-      if (y0 >= 0.0 && y0 <= 1.0 && t0 > 0.0 && t0 < bestT) {
-        bestT = t0;
-        bestFace = 0;
+      // consider() ignores t <= 0 (raytracer.go:287), so a root whose sign is
+      // known to be non-positive needs no division.
+      double n0 = -hb - sq, n1 = -hb + sq;
+      if (!t_nonpos(n0, a)) {
+        double t0 = n0 / a;
+        double y0 = l.o.y + l.d.y * t0;
+        if (y0 >= 0.0 && y0 <= 1.0 && t0 > 0.0 && t0 < bestT) {
+          bestT = t0;
+          bestFace = 0;
+        }
       }
-      double y1 = l.o.y + l.d.y * t1;
-      if (y1 >= 0.0 && y1 <= 1.0 && t1 > 0.0 && t1 < bestT) {
-        bestT = t1;
-        bestFace = 0;
+      if (!t_nonpos(n1, a)) {
+        double t1 = n1 / a;
+        double y1 = l.o.y + l.d.y * t1;
+        if (y1 >= 0.0 && y1 <= 1.0 && t1 > 0.0 && t1 < bestT) {
+          bestT = t1;
+          bestFace = 0;
+        }
       }
     }
   }
   if (__builtin_fabs(l.d.y) > 1e-12) {
-    double tTop = (1.0 - l.o.y) / l.d.y;
-    double px = l.o.x + l.d.x * tTop, pz = l.o.z + l.d.z * tTop;
-    if (px * px + pz * pz <= 1.0 && tTop > 0.0 && tTop < bestT) {
-      bestT = tTop;
-      bestFace = 1;
+    double nTop = 1.0 - l.o.y;
+    if (!t_nonpos(nTop, l.d.y)) {
+      double tTop = nTop / l.d.y;
+      double px = l.o.x + l.d.x * tTop, pz = l.o.z + l.d.z * tTop;
+      if (px * px + pz * pz <= 1.0 && tTop > 0.0 && tTop < bestT) {
+        bestT = tTop;
+        bestFace = 1;
+      }
     }
-    double tBot = -l.o.y / l.d.y;
-    px = l.o.x + l.d.x * tBot;
-    pz = l.o.z + l.d.z * tBot;
-    if (px * px + pz * pz <= 1.0 && tBot > 0.0 && tBot < bestT) {
-      bestT = tBot;
-      bestFace = 2;
+    double nBot = -l.o.y;
+    if (!t_nonpos(nBot, l.d.y)) {
+      double tBot = nBot / l.d.y;
+      double px = l.o.x + l.d.x * tBot, pz = l.o.z + l.d.z * tBot;
+      if (px * px + pz * pz <= 1.0 && tBot > 0.0 && tBot < bestT) {
+        bestT = tBot;
+        bestFace = 2;
+      }
     }
   }
   if (bestFace < 0) return false;
@@ -252,6 +296,48 @@ __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r,
 }
 
 __device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(__ballot(b)); }
+
+// Conservative FP32 test: can the segment o + t*d, 0 < t < tmax (d ~ unit)
+// come within the padded bounding sphere (centre c, radius^2 r2)? The exact
+// FP64 test can only report a hit whose point lies inside the object's
+// bounding sphere (to ~1e-12 relative); the host pads the radius by 0.01%
+// plus 1e-4*(1+|c|+|L|) and tmax carries 1e-4 relative slack, ~100x FP32
+// rounding at scene scales, so `false` proves the exact test misses (or, for
+// closestHit, cannot beat the current best).
+struct F3 {
+  float x, y, z;
+};
+__device__ __forceinline__ F3 f3(d3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
+__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g) {
+  const float* b = reinterpret_cast<const float*>(g + 12);
+  float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
+  float tc = ox * d.x + oy * d.y + oz * d.z;
+  tc = fminf(fmaxf(tc, 0.0f), tmax);
+  float qx = ox - tc * d.x, qy = oy - tc * d.y, qz = oz - tc * d.z;
+  return qx * qx + qy * qy + qz * qz <= b[3];
+}
+
+// Diagnostic build only (-DRT_PHASE_TIMING): wave cycles per phase, stamped
+// with s_memtime into per-wave scalar sums; never enabled in the product.
+#ifdef RT_PHASE_TIMING
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PH_BEGIN() uint64_t ph_t0_ = stamp()
+#define PH_MARK(k)              \
+  do {                          \
+    uint64_t t_ = stamp();      \
+    ph_acc[k] += t_ - ph_t0_;   \
+    ph_t0_ = t_;                \
+  } while (0)
+#else
+#define PH_BEGIN() (void)0
+#define PH_MARK(k) (void)0
+#endif
 
 // Frame stack: lane-interleaved so that one field of one frame is a
 // contiguous 512-B row for the wave.
@@ -284,7 +370,10 @@ struct View {
 };
 
 template <bool LDS>
-__global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ blob, Params P) {
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 3  // 168 VGPRs -> 3 waves/SIMD (measured best on C3/C4)
+#endif
+__global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char* __restrict__ blob, Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const char* base;
   if constexpr (LDS) {
@@ -326,6 +415,9 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
   bool exhausted = false;
   uint64_t c_shadow = 0, c_traced = 0, c_shaded = 0;
   uint64_t c_stest[4] = {0, 0, 0, 0};
+#ifdef RT_PHASE_TIMING
+  uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
   const double W1 = (double)(P.width - 1), H1 = (double)(P.height - 1);
 
@@ -342,7 +434,7 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
   // Propagate a finished traceRay colour up the lane's frame stack
   // (post-order, raytracer.go:528/554/557-561); ends with the lane either
   // tracing its next ray (pending refraction child / next sample) or idle.
-  auto unwind = [&](bool have_res, d3 res) {
+  auto unwind = [&](bool have_res, d3 res, bool pf_valid, long long pf_packed, d3 pf_lw, double pf_kr) {
     while (__any(have_res)) {
       if (have_res) {
         if (sp == 0) {
@@ -363,7 +455,11 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
           have_res = false;
         } else {
           double* f = frame_ptr(stk, sp - 1);
-          long long packed = __double_as_longlong(f[13 * 64]);
+          long long packed;
+          if (pf_valid)
+            packed = pf_packed;
+          else
+            packed = __double_as_longlong(f[13 * 64]);
           int fl = (int)(packed & 0xff);
           if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
             // reflection child done; trace the pending refraction child
@@ -384,14 +480,25 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
             } else {
               Tr = res;
             }
-            res = combine((fl & FL_TMODE) != 0, ld3(f, 0), mk(FM[0], FM[1], FM[2]), FM[3], f[12 * 64], R, Tr);
+            d3 lw;
+            double kr;
+            if (pf_valid) {
+              lw = pf_lw;
+              kr = pf_kr;
+            } else {
+              lw = ld3(f, 0);
+              kr = f[12 * 64];
+            }
+            res = combine((fl & FL_TMODE) != 0, lw, mk(FM[0], FM[1], FM[2]), FM[3], kr, R, Tr);
             sp--;
           }
+          pf_valid = false;
         }
       }
     }
   };
 
+  PH_BEGIN();
   for (;;) {
     // ---- refill idle lanes from the wave pool (one 8x8 tile per chunk) ----
     for (;;) {
@@ -435,18 +542,46 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
       }
       pool_next += take;
     }
+    PH_MARK(0);
     if (!__any(state != S_IDLE)) break;
 
     // ---- TRACE pass: closestHit over all objects (raytracer.go:469-483) ----
     if (__any(state == S_TRACE)) {
       const bool tr = state == S_TRACE;
+      // Prefetch the parent frame: a ray that misses pops it right after
+      // this pass, and the load latency hides under the object loop.
+      bool pf = false;
+      long long pf_packed = 0;
+      d3 pf_lw = mk(0, 0, 0);
+      double pf_kr = 0.0;
+#if RT_FRAME_PREFETCH
+      if (tr && sp > 0) {
+        const double* f = frame_ptr(stk, sp - 1);
+        pf = true;
+        pf_packed = __double_as_longlong(f[13 * 64]);
+        pf_lw = ld3(f, 0);
+        pf_kr = f[12 * 64];
+      }
+#endif
       bool found = false;
       double best_t = 0.0;
       int best_i = 0, best_f = 0;
+#if RT_CULL
+      const F3 of = f3(ray.o), df = f3(ray.d);
+#endif
       for (int i = 0; i < P.nobj; i++) {
         const int k = S.kind[i];
         const double* g = S.geo + (size_t)i * GEO;
-        if (tr) {
+        bool test = tr;
+#if RT_CULL
+        if (k != RT_PLANE) {
+          // an object entered beyond the lane's current best cannot win (strict <)
+          float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+          test = test && may_hit(of, df, tmax, g);
+          if (!__any(test)) continue;
+        }
+#endif
+        if (test) {
           double t;
           int f;
           if (object_hit(k, g, ray, t, f)) {
@@ -460,6 +595,7 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
         }
       }
       c_traced += popc_ballot(tr);
+      PH_MARK(1);
       d3 res = mk(0, 0, 0);
       if (tr) {
         if (found) {
@@ -472,7 +608,8 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
           res = lerp(mk(P.bg0[0], P.bg0[1], P.bg0[2]), mk(P.bg1[0], P.bg1[1], P.bg1[2]), t);
         }
       }
-      unwind(tr && !found, res);
+      unwind(tr && !found, res, pf, pf_packed, pf_lw, pf_kr);
+      PH_MARK(2);
     }
 
     // ---- SHADE pass, once enough lanes hold a hit ----
@@ -507,6 +644,7 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
     }
 
     // computeLighting + inShadow (raytracer.go:372-429)
+    PH_MARK(3);
     const double* M = S.mats + (size_t)mat * MAT;
     d3 L = mk(0, 0, 0);
     if (hit) L = scale(mk(P.amb[0], P.amb[1], P.amb[2]), M[9]);
@@ -522,12 +660,23 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
       Ray sr;
       sr.o = sorig;
       sr.d = ldir;
+#if RT_CULL
+      const F3 sof = f3(sorig), sdf = f3(ldir);
+      // occluders must lie within t < dist / |ray.d| (raytracer.go:424)
+      const float stmax = (float)(dist / rlen) * 1.0001f + 1e-4f;
+#endif
       for (int i = 0; i < P.nobj; i++) {
         if (!__any(open)) break;
         const int k = S.kind[i];
         const double* g = S.geo + (size_t)i * GEO;
         bool test = open && i != hit_i;
         c_stest[k] += popc_ballot(test);
+#if RT_CULL
+        if (k != RT_PLANE) {
+          test = test && may_hit(sof, sdf, stmax, g);
+          if (!__any(test)) continue;
+        }
+#endif
         if (test) {
           double t;
           int f;
@@ -536,6 +685,7 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
           }
         }
       }
+      PH_MARK(4);
       if (hit && open) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
         double ndl = go_max(0, dot(nw, ldir));
@@ -545,6 +695,7 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
         d3 specular = scale(lcol, M[10] * go_pow(spec, M[11]));
         L = add(add(L, diffuse), specular);
       }
+      PH_MARK(5);
     }
 
     // traceRay body after lighting (raytracer.go:505-561)
@@ -624,10 +775,15 @@ __global__ __launch_bounds__(WG) void rt_render_kernel(const char* __restrict__ 
         }
       }
     }
-    unwind(have_res, res);
+    PH_MARK(6);
+    unwind(have_res, res, false, 0, mk(0, 0, 0), 0.0);
+    PH_MARK(7);
   }
 
   if (lane == 0) {
+#ifdef RT_PHASE_TIMING
+    for (int k = 0; k < N_PHASE; k++) atomicAdd(P.stats + ST_PHASE + k, (unsigned long long)ph_acc[k]);
+#endif
     atomicAdd(P.stats + ST_TRACED, (unsigned long long)c_traced);
     atomicAdd(P.stats + ST_SHADOW, (unsigned long long)c_shadow);
     atomicAdd(P.stats + ST_SHADED, (unsigned long long)c_shaded);
@@ -976,6 +1132,28 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
         g[r * 4 + k] = w2o.m[r][k];
         sh[r * 4 + k] = o2w.m[r][k];
       }
+    if (o.kind != RT_PLANE) {
+      // World-space bounding sphere of the unit primitive: centre = O2W(local
+      // centre), radius <= ||L||_F * local radius (spectral <= Frobenius),
+      // padded for FP32 culling (see may_hit). Stored as 4 floats in 12..13.
+      const double lc[4][3] = {{0, 0, 0}, {0, 0, 0}, {0.5, 0.5, 0.5}, {0, 0.5, 0}};
+      const double lr[4] = {1.0, 0.0, 0.8660254037844387, 1.118033988749895};
+      double fro = 0.0;
+      for (int r = 0; r < 3; r++)
+        for (int k = 0; k < 3; k++) fro += o2w.m[r][k] * o2w.m[r][k];
+      fro = std::sqrt(fro);
+      double cc[3], cmax = 0.0;
+      for (int r = 0; r < 3; r++) {
+        cc[r] = o2w.m[r][0] * lc[o.kind][0] + o2w.m[r][1] * lc[o.kind][1] + o2w.m[r][2] * lc[o.kind][2] + o2w.m[r][3];
+        cmax = std::max(cmax, std::fabs(cc[r]));
+      }
+      double rad = fro * lr[o.kind] * 1.0001 + 1e-4 * (1.0 + cmax + fro);
+      float* b = reinterpret_cast<float*>(&g[12]);
+      b[0] = (float)cc[0];
+      b[1] = (float)cc[1];
+      b[2] = (float)cc[2];
+      b[3] = (float)(rad * rad);
+    }
     if (o.kind == RT_PLANE) {
       double nw[3], dv;
       plane_consts(w2o, o.plane_point, o.plane_normal, nw, &dv);
@@ -1069,7 +1247,7 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
   if (y0 < 0 || y1 > s.height || y1 <= y0) return fail(RT_E_INVALID, "rt_render_rows_async: bad row range");
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
-  const bool lds = s.blob_bytes <= LDS_MAX_BYTES;
+  const bool lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
   const int grid = lds ? c->grid_lds : c->grid_glb;
   Params P;
   std::memset(&P, 0, sizeof P);
@@ -1139,6 +1317,21 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
     out->shadow_tests[k] = h[ST_STESTS + k];
   }
   out->shaded_hits = h[ST_SHADED];
+#ifdef RT_PHASE_TIMING
+  {
+    unsigned long long ph[N_PHASE];
+    HIP_TRY(hipMemcpy(ph, c->stats + ST_PHASE, sizeof ph, hipMemcpyDeviceToHost));
+    unsigned long long tot = 0;
+    for (int k = 0; k < N_PHASE; k++) tot += ph[k];
+    if (tot) {
+      static const char* nm[N_PHASE] = {"refill", "trace_loop", "trace_unwind", "shade_surface",
+                                        "shadow_loops", "lighting", "material", "shade_unwind"};
+      fprintf(stderr, "[phase]");
+      for (int k = 0; k < N_PHASE; k++) fprintf(stderr, " %s=%.3f", nm[k], (double)ph[k] / (double)tot);
+      fprintf(stderr, " total_wave_cycles=%.4g\n", (double)tot);
+    }
+  }
+#endif
   float ms = 0.f;
   if (c->timed && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) out->kernel_ms = ms;
   if (reset) {
