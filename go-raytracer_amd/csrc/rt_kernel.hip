@@ -58,6 +58,9 @@
 #ifndef RT_CULL
 #define RT_CULL 1  // wave-uniform conservative bounding-sphere culling (exact, see may_hit)
 #endif
+#ifndef RT_LDS_FRAMES
+#define RT_LDS_FRAMES 0  // recursion levels whose frame core lives in LDS (measured: no gain)
+#endif
 #ifndef RT_CUBE_FAST
 #define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
 #endif
@@ -78,7 +81,12 @@ using namespace rt;
 // kind   [nobj] int32;  objmat [nobj][OMAT] int32 per-face material index
 // ---------------------------------------------------------------------------
 enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8 };
-enum { FRAME_FIELDS = 14 };  // Lw[3] cfirst[3] pend_o[3] pend_d[3] kr packed
+// Frame of one traceRay activation that has children (post-order combine).
+// Global layout: 14 fields, lane-interleaved: Lw[3] cfirst[3] pend_o[3]
+// pend_d[3] kr packed. The CORE fields (Lw, kr, packed) of the first
+// RT_LDS_FRAMES levels live in LDS instead; cfirst/pending (only used when a
+// material is both reflective and transparent) always live in HBM.
+enum { FRAME_FIELDS = 14, CORE = 5 };
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_COUNT = 7, ST_PHASE = 16, N_PHASE = 8 };
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
@@ -88,6 +96,7 @@ enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
 enum { LDS_MAX_BYTES = RT_LDS_MAX };
 
 struct Params {
+  int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
   int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, blob_bytes;
   const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
   unsigned int* queue;
@@ -351,6 +360,9 @@ __device__ __forceinline__ d3 ld3(const double* f, int field) {
   return mk(f[(field + 0) * 64], f[(field + 1) * 64], f[(field + 2) * 64]);
 }
 
+// CORE field c (0..2 Lw, 3 kr, 4 packed) -> global field index.
+__device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ? 12 : 13); }
+
 // Frame flags (packed with the material index).
 enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8 };
 
@@ -397,10 +409,24 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   const int lane = (int)(threadIdx.x & 63);
   const int wslot = (int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
   double* stk = P.stack + (size_t)wslot * ((size_t)P.frames * FRAME_FIELDS * 64) + lane;
+  double* lfr = reinterpret_cast<double*>(smem + P.lds_frames_off) +
+                (size_t)(threadIdx.x >> 6) * (RT_LDS_FRAMES * CORE * 64) + lane;
+  // frame core accessors: level < RT_LDS_FRAMES in LDS, deeper in HBM
+  auto core_ld = [&](int level, int c) -> double {
+    if (level < RT_LDS_FRAMES) return lfr[(level * CORE + c) * 64];
+    return frame_ptr(stk, level)[core_gfield(c) * 64];
+  };
+  auto core_st = [&](int level, int c, double v) {
+    if (level < RT_LDS_FRAMES)
+      lfr[(level * CORE + c) * 64] = v;
+    else
+      frame_ptr(stk, level)[core_gfield(c) * 64] = v;
+  };
   const d3 eye = mk(0.0, 0.0, -1.0);  // raytracer.go:605-609
 
   // lane state
   int state = S_IDLE;
+  bool need_gen = false;  // lane waits for its next sample ray
   int px = 0, py = 0, sample = 0, sp = 0;
   int hit_i = 0, hit_f = 0;
   double hit_t = 0.0;
@@ -449,7 +475,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                 (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
             state = S_IDLE;
           } else {
-            gen_ray();
+            need_gen = true;  // next sample ray, generated in one uniform block
             state = S_TRACE;
           }
           have_res = false;
@@ -459,12 +485,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           if (pf_valid)
             packed = pf_packed;
           else
-            packed = __double_as_longlong(f[13 * 64]);
+            packed = __double_as_longlong(core_ld(sp - 1, 4));
           int fl = (int)(packed & 0xff);
           if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
             // reflection child done; trace the pending refraction child
             st3(f, 3, res);
-            f[13 * 64] = __longlong_as_double(packed | FL_STAGE);
+            core_st(sp - 1, 4, __longlong_as_double(packed | FL_STAGE));
             ray.o = ld3(f, 6);
             ray.d = ld3(f, 9);
             state = S_TRACE;
@@ -486,8 +512,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               lw = pf_lw;
               kr = pf_kr;
             } else {
-              lw = ld3(f, 0);
-              kr = f[12 * 64];
+              lw = mk(core_ld(sp - 1, 0), core_ld(sp - 1, 1), core_ld(sp - 1, 2));
+              kr = core_ld(sp - 1, 3);
             }
             res = combine((fl & FL_TMODE) != 0, lw, mk(FM[0], FM[1], FM[2]), FM[3], kr, R, Tr);
             sp--;
@@ -536,14 +562,21 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           sample = 0;
           sum = mk(0, 0, 0);
           sp = 0;
-          gen_ray();
+          need_gen = true;
           state = S_TRACE;
         }
       }
       pool_next += take;
     }
-    PH_MARK(0);
     if (!__any(state != S_IDLE)) break;
+    // ---- new sample rays for every lane that needs one, in one block ----
+    if (__any(need_gen)) {
+      if (need_gen) {
+        gen_ray();
+        need_gen = false;
+      }
+    }
+    PH_MARK(0);
 
     // ---- TRACE pass: closestHit over all objects (raytracer.go:469-483) ----
     if (__any(state == S_TRACE)) {
@@ -556,11 +589,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       double pf_kr = 0.0;
 #if RT_FRAME_PREFETCH
       if (tr && sp > 0) {
-        const double* f = frame_ptr(stk, sp - 1);
         pf = true;
-        pf_packed = __double_as_longlong(f[13 * 64]);
-        pf_lw = ld3(f, 0);
-        pf_kr = f[12 * 64];
+        pf_packed = __double_as_longlong(core_ld(sp - 1, 4));
+        pf_lw = mk(core_ld(sp - 1, 0), core_ld(sp - 1, 1), core_ld(sp - 1, 2));
+        pf_kr = core_ld(sp - 1, 3);
       }
 #endif
       bool found = false;
@@ -756,16 +788,18 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         }
         const int d = P.depth - sp;  // depth of the current ray
         if (d - 1 > 0 && (hasR || hasT)) {
-          double* f = frame_ptr(stk, sp);
-          st3(f, 0, lw);
+          core_st(sp, 0, lw.x);
+          core_st(sp, 1, lw.y);
+          core_st(sp, 2, lw.z);
           if (hasR && hasT) {
+            double* f = frame_ptr(stk, sp);
             st3(f, 6, trr.o);
             st3(f, 9, trr.d);
           }
-          f[12 * 64] = kr;
+          core_st(sp, 3, kr);
           long long packed =
               ((long long)mat << 8) | (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
-          f[13 * 64] = __longlong_as_double(packed);
+          core_st(sp, 4, __longlong_as_double(packed));
           sp++;
           ray = hasR ? rr : trr;
           state = S_TRACE;
@@ -967,6 +1001,7 @@ struct rt_context {
   unsigned long long* stats = nullptr;
   double* stack = nullptr;
   size_t stack_bytes = 0;
+  int stack_waves = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   uint64_t primary_pending = 0;  // host-side count of launched primary rays
@@ -1223,7 +1258,8 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   s.kinds = kind;
   // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
   int frames = std::max(1, s.depth - 1);
-  size_t need = (size_t)std::max(c->grid_lds, c->grid_glb) * WAVES_PER_WG * frames * FRAME_FIELDS * 64 * sizeof(double);
+  const int waves = c->cus * 8 * WAVES_PER_WG;  // upper bound of any persistent grid
+  size_t need = (size_t)waves * frames * FRAME_FIELDS * 64 * sizeof(double);
   if (need > c->stack_bytes) {
     (void)hipFree(c->stack);
     c->stack = nullptr;
@@ -1234,6 +1270,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     }
     c->stack_bytes = need;
   }
+  c->stack_waves = (int)(c->stack_bytes / ((size_t)frames * FRAME_FIELDS * 64 * sizeof(double)));
   free_scene(c->sc);
   c->sc = s;
   c->has_scene = true;
@@ -1248,9 +1285,22 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
   const bool lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
-  const int grid = lds ? c->grid_lds : c->grid_glb;
+  const int frames_off = lds ? s.blob_bytes : 0;
+  const int shmem = frames_off + WAVES_PER_WG * RT_LDS_FRAMES * CORE * 64 * (int)sizeof(double);
+  int per_cu = 0;
+  if (lds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, WG, shmem) != hipSuccess)
+      per_cu = 0;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false>, WG, shmem) != hipSuccess)
+      per_cu = 0;
+  }
+  if (per_cu <= 0) per_cu = 1;
+  const int grid = c->cus * std::min(per_cu, 8);
+  if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
   Params P;
   std::memset(&P, 0, sizeof P);
+  P.lds_frames_off = frames_off;
   P.off_geo = s.off_geo;
   P.off_shade = s.off_shade;
   P.off_mats = s.off_mats;
@@ -1287,9 +1337,9 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
   HIP_TRY(hipMemsetAsync(c->queue, 0, 256, st));
   HIP_TRY(hipEventRecord(c->ev0, st));
   if (lds)
-    hipLaunchKernelGGL(rt_render_kernel<true>, dim3(grid), dim3(WG), s.blob_bytes, st, (const char*)s.blob, P);
+    hipLaunchKernelGGL(rt_render_kernel<true>, dim3(grid), dim3(WG), shmem, st, (const char*)s.blob, P);
   else
-    hipLaunchKernelGGL(rt_render_kernel<false>, dim3(grid), dim3(WG), 0, st, (const char*)s.blob, P);
+    hipLaunchKernelGGL(rt_render_kernel<false>, dim3(grid), dim3(WG), shmem, st, (const char*)s.blob, P);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   c->timed = true;

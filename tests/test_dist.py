@@ -1,0 +1,77 @@
+"""Row-band sharding + gather to rank 0 (go_raytracer_amd/dist.py) on CPU with
+gloo, world sizes 2 and 3 (uneven bands). Each rank renders its band with the
+CPU oracle; the assembled frame must equal the single-process full frame --
+the property the GPU path relies on (RNG depends only on (x, 20-row strip),
+raytracer.go:627-634)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, w, h, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    import oracle_bind
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    packed = pkg.scene.convert(pkg.configs.c2(width=w, height=h))
+    y0, y1, per = pkg.dist.band_rows(h, rank, world)
+    band = torch.zeros((per, w, 4), dtype=torch.uint8)
+    if y1 > y0:
+        img, _ = oracle_bind.render_rows(packed, y0, y1, threads=2)
+        band[: y1 - y0] = torch.from_numpy(img)
+    frame = pkg.dist.gather_frame(band, h)
+    if rank == 0:
+        q.put(frame.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,w,h", [(2, 64, 40), (3, 48, 31)])
+def test_gather_of_row_bands_equals_full_frame(world, w, h):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind
+    import go_raytracer_amd as rt
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full, _ = oracle_bind.render_rows(rt.scene.convert(rt.configs.c2(width=w, height=h)))
+    assert frame.shape == full.shape
+    assert np.array_equal(frame, full)
+
+
+def test_band_rows_cover_the_frame_once():
+    import go_raytracer_amd as rt
+    for h in (1, 7, 20, 2160, 4321):
+        for world in (1, 2, 3, 4, 8):
+            rows = []
+            for r in range(world):
+                y0, y1, per = rt.dist.band_rows(h, r, world)
+                assert 0 <= y0 <= y1 <= h and y1 - y0 <= per
+                rows.extend(range(y0, y1))
+            assert rows == list(range(h))
