@@ -38,7 +38,19 @@ def parse():
     p.add_argument("--height", type=int, default=None)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=8)
+    p.add_argument("--shard", choices=["interleaved", "bands"], default="interleaved")
     return p.parse_args()
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch of the render kernel from the committed rocprofv3
+    --pmc passes (profiles/traffic_<config>.json, scripts/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "traffic_%s.json" % config)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes"), os.path.relpath(path, ROOT)
 
 
 def cpu_baseline(packed, threads):
@@ -81,7 +93,7 @@ def main():
     packed = pkg.scene.convert(rargs)
     ctx = pkg.RenderContext(local)
     ctx.set_scene(packed)
-    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev)
+    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=args.shard)
 
     def barrier():
         if world > 1:
@@ -98,7 +110,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         dr.step()
-        if dr.y1 > dr.y0:
+        if dr.has_work():
             kernel_ms.append(ctx.last_kernel_ms())
     torch.cuda.synchronize()
     barrier()
@@ -128,7 +140,7 @@ def main():
         # launch / average launch duration (HIP events on the launch stream)
         flops_per_launch = flops_local / max(1, len(kernel_ms))
         achieved_tf = flops_per_launch / (kavg * 1e-3) / 1e12 if kavg > 0 else 0.0
-        out_bytes = (dr.y1 - dr.y0) * packed.width * 4
+        out_bytes = dr.buf.numel()
         line = {
             "metric": "Mrays/s (primary+shadow+reflect) at 4K depth=6",
             "value": round(value, 2),
@@ -142,18 +154,23 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "%s: %s" % (args.config, (cfg.__doc__ or "").split(".")[0].strip()),
+            "config": {"workload": "%s: %s" % (args.config, pkg.configs.WORKLOADS[args.config]),
                        "width": packed.width, "height": packed.height, "depth": rargs.depth,
                        "lights": len(rargs.lights), "objects": int(packed.scene.num_objects),
-                       "rays_per_frame": int(per_step_rays), "parallelism": "rows%d" % world},
+                       "rays_per_frame": int(per_step_rays),
+                       "parallelism": "rows%d-%s" % (world, args.shard)},
             "roofline": {"bound": "valu-fp64", "achieved": round(achieved_tf, 3), "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
                          "frac_nofma_ceiling": round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),
                          "kernel_ms": round(kavg, 4), "flops_per_launch": int(flops_per_launch),
                          "hbm_out_gbs": round(out_bytes / (kavg * 1e-3) / 1e9, 2) if kavg > 0 else None,
-                         "traffic": None},
+                         "traffic": None, "traffic_source": None},
             "cpu_baseline": None,
         }
+        tb, src = pmc_traffic(args.config)
+        if tb is not None and world == 1 and not args.width and not args.height:
+            line["roofline"]["traffic"] = int(tb)
+            line["roofline"]["traffic_source"] = src
         if world == 1 and args.cpu_baseline == "auto":
             line["cpu_baseline"] = cpu_baseline(packed, args.cpu_threads)
         print(json.dumps(line), flush=True)

@@ -129,3 +129,12 @@ def c5(width=7680, height=4320, nx=100, ny=100, nz=10):
 
 
 CONFIGS = {"canned": canned, "c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}
+
+WORKLOADS = {
+    "canned": "canned.gml 1900x1200 depth 7 (reference golden example_canned.png)",
+    "c1": "1 sphere, 1 light, 256x256, depth 1",
+    "c2": "3 spheres (mirror, fuzzy, glass) + plane, 2 lights, 1920x1080, depth 4",
+    "c3": "cylinder + cube + sphere (cone substitute) over a reflective plane, 4 lights, 3840x2160, depth 6",
+    "c4": "cube U 64 spheres (CSG substitute) + plane, 2 lights, 3840x2160, depth 8",
+    "c5": "100k spheres + plane, 2 lights, 7680x4320, depth 8",
+}

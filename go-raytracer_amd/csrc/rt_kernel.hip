@@ -104,6 +104,7 @@ struct Params {
   double* stack;
   uint32_t* out;
   int width, height, depth, nobj, nlights, y0, y1, tiles_x;
+  int trow0, trow_stride;  // trow_stride > 0: output tile row j renders image tile row trow0 + j*stride
   unsigned int total_slots;
   int frames;  // stack frames per lane (depth - 1, >= 1)
   double vw, vh;
@@ -428,6 +429,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   int state = S_IDLE;
   bool need_gen = false;  // lane waits for its next sample ray
   int px = 0, py = 0, sample = 0, sp = 0;
+  unsigned int pout = 0;  // output pixel index
   int hit_i = 0, hit_f = 0;
   double hit_t = 0.0;
   Pcg rng{0, 0};
@@ -471,7 +473,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
             uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
             uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
-            P.out[(size_t)(py - P.y0) * (size_t)P.width + (size_t)px] =
+            P.out[pout] =
                 (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
             state = S_IDLE;
           } else {
@@ -548,11 +550,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if (need && rank < take) {
         unsigned int slot = pool_next + rank;
         unsigned int tile = slot / (TILE * TILE), within = slot % (TILE * TILE);
-        int x = (int)((tile % (unsigned)P.tiles_x) * TILE + within % TILE);
-        int y = P.y0 + (int)((tile / (unsigned)P.tiles_x) * TILE + within / TILE);
+        const int trow = (int)(tile / (unsigned)P.tiles_x);
+        const int x = (int)((tile % (unsigned)P.tiles_x) * TILE + within % TILE);
+        const int orow = trow * TILE + (int)(within / TILE);
+        const int y = P.trow_stride > 0 ? (P.trow0 + trow * P.trow_stride) * TILE + (int)(within / TILE) : P.y0 + orow;
         if (x < P.width && y < P.y1) {
           px = x;
           py = y;
+          pout = (unsigned int)orow * (unsigned int)P.width + (unsigned int)x;
           // rng = PCG(0xDEAD^x, 0xBEEF^ymin) advanced 8*(y%20) draws
           // (raytracer.go:632-643: 2 draws per sample, 4 samples per row).
           int ymin = y - y % 20;
@@ -1277,11 +1282,10 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   return RT_OK;
 }
 
-int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stream) {
-  if (!c || !c->has_scene) return fail(RT_E_INVALID, "rt_render_rows_async: no scene set");
-  if (!d_rgba) return fail(RT_E_INVALID, "rt_render_rows_async: NULL output");
+// Shared launch: contiguous rows [y0, y1) (stride == 0) or `ntrows` 8-row tile
+// rows starting at tile row trow0 with stride `stride` (y0 = 0, y1 = height).
+static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntrows, void* d_rgba, void* stream) {
   const DevScene& s = c->sc;
-  if (y0 < 0 || y1 > s.height || y1 <= y0) return fail(RT_E_INVALID, "rt_render_rows_async: bad row range");
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
   const bool lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
@@ -1320,8 +1324,10 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
   P.nlights = s.nlights;
   P.y0 = y0;
   P.y1 = y1;
+  P.trow0 = trow0;
+  P.trow_stride = stride;
   P.tiles_x = (s.width + TILE - 1) / TILE;
-  int tiles_y = (y1 - y0 + TILE - 1) / TILE;
+  int tiles_y = stride > 0 ? ntrows : (y1 - y0 + TILE - 1) / TILE;
   size_t slots = (size_t)P.tiles_x * tiles_y * TILE * TILE;
   if (slots >= 0xFFFFFFFFull - 2u * CHUNK * (size_t)grid * WAVES_PER_WG)
     return fail(RT_E_INVALID, "image too large for one launch");
@@ -1343,9 +1349,33 @@ int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stre
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   c->timed = true;
-  c->primary_pending += (uint64_t)4 * (uint64_t)s.width * (uint64_t)(y1 - y0);
+  uint64_t rows = 0;
+  if (stride > 0) {
+    for (int j = 0; j < ntrows; j++) {
+      int r0 = (trow0 + j * stride) * TILE;
+      rows += (uint64_t)std::max(0, std::min((int)TILE, s.height - r0));
+    }
+  } else {
+    rows = (uint64_t)(y1 - y0);
+  }
+  c->primary_pending += (uint64_t)4 * (uint64_t)s.width * rows;
   return RT_OK;
 }
+
+int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stream) {
+  if (!c || !c->has_scene) return fail(RT_E_INVALID, "rt_render_rows_async: no scene set");
+  if (!d_rgba) return fail(RT_E_INVALID, "rt_render_rows_async: NULL output");
+  if (y0 < 0 || y1 > c->sc.height || y1 <= y0) return fail(RT_E_INVALID, "rt_render_rows_async: bad row range");
+  return launch(c, y0, y1, 0, 0, 0, d_rgba, stream);
+}
+
+int rt_render_tile_rows_async(rt_context* c, int trow0, int trow_stride, int ntrows, void* d_rgba, void* stream) {
+  if (!c || !c->has_scene) return fail(RT_E_INVALID, "rt_render_tile_rows_async: no scene set");
+  if (!d_rgba) return fail(RT_E_INVALID, "rt_render_tile_rows_async: NULL output");
+  if (trow0 < 0 || trow_stride <= 0 || ntrows <= 0) return fail(RT_E_INVALID, "rt_render_tile_rows_async: bad tile rows");
+  return launch(c, 0, c->sc.height, trow0, trow_stride, ntrows, d_rgba, stream);
+}
+
 
 int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
   if (!c || !out) return fail(RT_E_INVALID, "rt_read_stats: NULL argument");

@@ -1,71 +1,99 @@
-"""Row-band sharding of one frame across GPUs + gather to rank 0 (RCCL/xGMI).
+"""Sharding one frame across GPUs + gather to rank 0 (RCCL over xGMI).
 
 Pixels are independent and the jitter RNG depends only on (column, 20-row
 strip) (raytracer.go:627-634), so any row partition renders bit-identical
-rows. One process per GPU; rank r renders rows [r*B, min(H, (r+1)*B)) with
-B = ceil(H / world). The frame is assembled on rank 0 with one gather over
-the process group (backend "nccl" = RCCL on ROCm; "gloo" on CPU tests). No
-reduction is needed.
+rows. One process per GPU. Two partitions:
+
+- "interleaved" (default): the image's 8-row tile rows are dealt round-robin,
+  rank r owning tile rows r, r+N, r+2N, ... -- sky and ground rows are spread
+  evenly, so ranks finish together. Rank 0 gathers the [K*8, W, 4] slabs and
+  de-interleaves them on the device.
+- "bands": contiguous bands of ceil(H/N) rows (simple; imbalanced when the
+  cost varies with height).
+
+The gather is one collective over the process group (backend "nccl" = RCCL on
+ROCm; "gloo" in the CPU tests). No reduction is needed.
 """
 import math
 
+TILE = 8
+
 
 def band_rows(height, rank, world):
-    """Rows [y0, y1) owned by `rank` (the last band may be shorter or empty)."""
+    """Contiguous band [y0, y1) owned by `rank` (last band may be shorter/empty)."""
     per = int(math.ceil(height / float(world)))
     y0 = min(height, rank * per)
     y1 = min(height, y0 + per)
     return y0, y1, per
 
 
-def assemble(bands, height):
-    """Concatenate per-rank band buffers ([per, W, 4] each, padded) into [H, W, 4]."""
-    import torch
-    world = len(bands)
-    per = bands[0].shape[0]
-    full = torch.cat(list(bands), dim=0)
-    assert full.shape[0] == per * world
+def tile_rows(height, world):
+    """(tile rows in the image, tile rows per rank K): rank r owns tile rows
+    r + j*world for j < K (those past the image are padding)."""
+    nt = (height + TILE - 1) // TILE
+    return nt, (nt + world - 1) // world
+
+
+def deinterleave(slabs, height):
+    """slabs: [world, K*8, W, 4] (rank-major) -> [height, W, 4] frame."""
+    world, rows, W, ch = slabs.shape
+    K = rows // TILE
+    full = slabs.reshape(world, K, TILE, W, ch).permute(1, 0, 2, 3, 4).reshape(K * world * TILE, W, ch)
     return full[:height]
 
 
-def gather_frame(band_buf, height, group=None):
-    """Gather every rank's padded band to rank 0. Returns the [H, W, 4] frame on
-    rank 0 and None elsewhere."""
+def gather_frame(buf, height, mode="bands", group=None):
+    """Gather every rank's buffer to rank 0 and assemble the [H, W, 4] frame
+    there (None elsewhere)."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world == 1:
-        return band_buf[:height]
+        return deinterleave(buf.unsqueeze(0), height) if mode == "interleaved" else buf[:height]
+    rank = dist.get_rank(group)
     if rank == 0:
-        bufs = [torch.empty_like(band_buf) for _ in range(world)]
-        dist.gather(band_buf, gather_list=bufs, dst=0, group=group)
-        return assemble(bufs, height)
-    dist.gather(band_buf, dst=0, group=group)
+        bufs = [torch.empty_like(buf) for _ in range(world)]
+        dist.gather(buf, gather_list=bufs, dst=0, group=group)
+        stacked = torch.stack(bufs, 0)
+        if mode == "interleaved":
+            return deinterleave(stacked, height)
+        return stacked.reshape(-1, *buf.shape[1:])[:height]
+    dist.gather(buf, dst=0, group=group)
     return None
 
 
 class DistributedRenderer:
     """Renders one frame per step with rows sharded over the process group."""
 
-    def __init__(self, ctx, packed, rank, world, device):
+    def __init__(self, ctx, packed, rank, world, device, mode="interleaved"):
         import torch
         self.ctx = ctx
         self.packed = packed
         self.rank = rank
         self.world = world
+        self.mode = mode
         self.H = packed.height
         self.W = packed.width
-        self.y0, self.y1, self.per = band_rows(self.H, rank, world)
-        self.band = torch.zeros((self.per, self.W, 4), dtype=torch.uint8, device=device)
+        if mode == "interleaved":
+            self.nt, self.K = tile_rows(self.H, world)
+            # this rank's valid tile rows (the rest of its slab is padding)
+            self.ntrows = max(0, min(self.K, (self.nt - rank + world - 1) // world))
+            rows = self.K * TILE
+        else:
+            self.y0, self.y1, rows = band_rows(self.H, rank, world)
+        self.buf = torch.zeros((rows, self.W, 4), dtype=torch.uint8, device=device)
         self.frame = None
 
+    def has_work(self):
+        return self.ntrows > 0 if self.mode == "interleaved" else self.y1 > self.y0
+
     def step(self, gather=True):
-        n = self.y1 - self.y0
-        if n > 0:
-            self.ctx.render_rows_async(self.y0, self.y1, self.band[:n])
-        if gather and self.world > 1:
-            self.frame = gather_frame(self.band, self.H)
-        elif self.world == 1:
-            self.frame = self.band
+        if self.mode == "interleaved":
+            if self.ntrows > 0:
+                self.ctx.render_tile_rows_async(self.rank, self.world, self.ntrows,
+                                                self.buf[: self.ntrows * TILE])
+        elif self.y1 > self.y0:
+            self.ctx.render_rows_async(self.y0, self.y1, self.buf[: self.y1 - self.y0])
+        if gather:
+            self.frame = gather_frame(self.buf, self.H, self.mode)
         return self.frame

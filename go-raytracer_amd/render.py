@@ -43,6 +43,8 @@ def load_library(path=LIB_PATH):
     l.rt_set_scene.restype = i
     l.rt_render_rows_async.argtypes = [vp, i, i, vp, vp]
     l.rt_render_rows_async.restype = i
+    l.rt_render_tile_rows_async.argtypes = [vp, i, i, i, vp, vp]
+    l.rt_render_tile_rows_async.restype = i
     l.rt_read_stats.argtypes = [vp, vp, i, vp]
     l.rt_read_stats.restype = i
     l.rt_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
@@ -108,6 +110,18 @@ class RenderContext:
         s = torch.cuda.current_stream(self.device) if stream is None else stream
         _check(self.lib.rt_render_rows_async(self.handle, int(y0), int(y1), C.c_void_p(out.data_ptr()),
                                              C.c_void_p(s.cuda_stream)), "rt_render_rows_async")
+
+    def render_tile_rows_async(self, trow0, stride, ntrows, out, stream=None):
+        """Enqueue `ntrows` interleaved 8-row tile rows (image tile rows trow0 + j*stride)
+        into the uint8 CUDA tensor `out` ([ntrows*8, W, 4])."""
+        torch = self.torch
+        W = self.packed.width
+        assert out.dtype == torch.uint8 and out.is_cuda and out.is_contiguous()
+        assert out.numel() == ntrows * 8 * W * 4, "output tensor shape does not match tile rows"
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
+        _check(self.lib.rt_render_tile_rows_async(self.handle, int(trow0), int(stride), int(ntrows),
+                                                  C.c_void_p(out.data_ptr()), C.c_void_p(s.cuda_stream)),
+               "rt_render_tile_rows_async")
 
     def read_stats(self, reset=True, stream=None):
         s = self.torch.cuda.current_stream(self.device) if stream is None else stream

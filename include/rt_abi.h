@@ -159,6 +159,14 @@ int rt_set_scene(rt_context *ctx, const rt_scene *scene);
 int rt_render_rows_async(rt_context *ctx, int y0, int y1, void *d_rgba,
                          void *stream);
 
+/* Interleaved variant for load-balanced multi-GPU sharding: render `ntrows`
+ * 8-row tile rows, output tile row j being image rows
+ * [(trow0 + j*trow_stride)*8, +8) clipped to the image, into d_rgba packed
+ * contiguously (output row j*8 + r, stride 4*width; rows past the image are
+ * left untouched). Same pixels as a full-frame render. */
+int rt_render_tile_rows_async(rt_context *ctx, int trow0, int trow_stride, int ntrows,
+                              void *d_rgba, void *stream);
+
 /* Read (and optionally reset) the work counters accumulated on the device
  * since the last reset. Synchronises the given stream. */
 int rt_read_stats(rt_context *ctx, void *stream, int reset, rt_stats *out);

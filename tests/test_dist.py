@@ -21,7 +21,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, w, h, q):
+def _worker(rank, world, port, w, h, q, mode="bands"):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -32,20 +32,31 @@ def _worker(rank, world, port, w, h, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     packed = pkg.scene.convert(pkg.configs.c2(width=w, height=h))
-    y0, y1, per = pkg.dist.band_rows(h, rank, world)
-    band = torch.zeros((per, w, 4), dtype=torch.uint8)
-    if y1 > y0:
-        img, _ = oracle_bind.render_rows(packed, y0, y1, threads=2)
-        band[: y1 - y0] = torch.from_numpy(img)
-    frame = pkg.dist.gather_frame(band, h)
+    if mode == "bands":
+        y0, y1, per = pkg.dist.band_rows(h, rank, world)
+        band = torch.zeros((per, w, 4), dtype=torch.uint8)
+        if y1 > y0:
+            img, _ = oracle_bind.render_rows(packed, y0, y1, threads=2)
+            band[: y1 - y0] = torch.from_numpy(img)
+    else:  # interleaved 8-row tile rows r, r+world, ...
+        nt, K = pkg.dist.tile_rows(h, world)
+        band = torch.zeros((K * 8, w, 4), dtype=torch.uint8)
+        for j in range(K):
+            t = rank + j * world
+            if t < nt:
+                y0, y1 = t * 8, min(h, t * 8 + 8)
+                img, _ = oracle_bind.render_rows(packed, y0, y1, threads=2)
+                band[j * 8: j * 8 + (y1 - y0)] = torch.from_numpy(img)
+    frame = pkg.dist.gather_frame(band, h, mode)
     if rank == 0:
         q.put(frame.numpy().copy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,w,h", [(2, 64, 40), (3, 48, 31)])
-def test_gather_of_row_bands_equals_full_frame(world, w, h):
+@pytest.mark.parametrize("world,w,h,mode", [(2, 64, 40, "bands"), (3, 48, 31, "bands"),
+                                            (2, 64, 40, "interleaved"), (3, 40, 45, "interleaved")])
+def test_gather_of_row_bands_equals_full_frame(world, w, h, mode):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind
@@ -53,7 +64,7 @@ def test_gather_of_row_bands_equals_full_frame(world, w, h):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     frame = q.get(timeout=120)

@@ -130,3 +130,19 @@ def test_singular_transform_is_rejected(ctx):
     args = rt.scene.RenderArgs(ambient=(0, 0, 0), lights=[], scene=bad, depth=1, fov=90.0, width=8, height=8)
     with pytest.raises(rt.render.RenderError):
         ctx.set_scene(rt.scene.convert(args))
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_interleaved_tile_rows_equal_full_frame(ctx, world):
+    import torch
+    packed = rt.scene.convert(rt.configs.c3(width=320, height=180))
+    full, _ = render(ctx, packed)
+    nt, K = rt.dist.tile_rows(180, world)
+    slabs = torch.zeros((world, K * 8, 320, 4), dtype=torch.uint8, device="cuda")
+    for r in range(world):
+        n = max(0, min(K, (nt - r + world - 1) // world))
+        if n:
+            ctx.render_tile_rows_async(r, world, n, slabs[r, : n * 8])
+    torch.cuda.synchronize()
+    frame = rt.dist.deinterleave(slabs, 180).cpu().numpy()
+    assert_same(frame, full, "interleaved world %d" % world)
