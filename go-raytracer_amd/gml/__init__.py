@@ -1,0 +1,23 @@
+"""Host GML front end: lexer, parser, evaluator, RenderArgs
+dumps. Runs GML programs once per frame on the host and hands RenderArgs to
+the renderer through the `render` hook, exactly like the reference's
+EvalState.Render (internal/gml/evaluator.go:48)."""
+from .evaluator import EvalState, GMLError, SurfaceFn, eval_surface_fn  # noqa: F401
+from .printer import render_args_lines  # noqa: F401
+from .syntax import ParseError  # noqa: F401
+
+
+def run_file(path):
+    """Evaluate a .gml file; returns the list of RenderArgs it rendered (in order)
+    and the final EvalState."""
+    out = []
+    st = EvalState(render=lambda e, a: out.append((a, e)))
+    st.parse_and_eval_file(path)
+    return out, st
+
+
+def run_text(text):
+    out = []
+    st = EvalState(render=lambda e, a: out.append((a, e)))
+    st.parse_and_eval(text)
+    return out, st

@@ -176,6 +176,11 @@ def flatten(root):
 def _face_materials(obj, kind):
     s = obj.surface
     n = _NFACES[kind]
+    if hasattr(s, "closure") and hasattr(s, "material"):  # gml.SurfaceFn
+        if s.material is not None:
+            s = s.material
+        else:
+            return [s] * n
     if isinstance(s, Material):
         return [s] * n
     s = tuple(s)
