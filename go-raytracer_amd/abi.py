@@ -60,6 +60,13 @@ class rt_scene(C.Structure):
         ("materials", C.POINTER(rt_material)),
         ("num_objects", C.c_int32),
         ("num_materials", C.c_int32),
+        ("program_code", C.POINTER(C.c_uint32)),
+        ("program_consts", C.POINTER(C.c_uint64)),
+        ("program_entry", C.POINTER(C.c_int32)),
+        ("num_programs", C.c_int32),
+        ("program_code_words", C.c_int32),
+        ("program_const_count", C.c_int32),
+        ("reserved0", C.c_int32),
     ]
 
 
@@ -71,6 +78,7 @@ class rt_stats(C.Structure):
         ("tests", C.c_uint64 * RT_NUM_KINDS),
         ("shadow_tests", C.c_uint64 * RT_NUM_KINDS),
         ("shaded_hits", C.c_uint64),
+        ("surface_errors", C.c_uint64),
         ("kernel_ms", C.c_double),
     ]
 
@@ -82,6 +90,7 @@ class rt_stats(C.Structure):
             "tests": [int(v) for v in self.tests],
             "shadow_tests": [int(v) for v in self.shadow_tests],
             "shaded_hits": int(self.shaded_hits),
+            "surface_errors": int(self.surface_errors),
         }
 
     def total_rays(self):
@@ -91,11 +100,13 @@ class rt_stats(C.Structure):
 class PackedScene:
     """Owns the ctypes arrays an rt_scene points into (keeps them alive)."""
 
-    def __init__(self, scene, lights, objects, materials):
+    def __init__(self, scene, lights, objects, materials, programs=None):
         self.scene = scene
         self._lights = lights
         self._objects = objects
         self._materials = materials
+        # (code, consts, entry ctypes arrays, [(SurfaceFn, EvalState stack)] per program)
+        self.programs = programs
 
     @property
     def width(self):

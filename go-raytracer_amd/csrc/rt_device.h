@@ -179,6 +179,104 @@ __device__ __forceinline__ Pcg pcg_jump(Pcg s, uint64_t ahi, uint64_t alo, uint6
   return Pcg{hi, lo2};
 }
 
+// int64(v) for float64 v on amd64 (CVTTSD2SQ): MinInt64 on NaN/overflow.
+__device__ __forceinline__ long long go_f2i(double v) {
+  if (!(v >= -9223372036854775808.0 && v < 9223372036854775808.0)) return (long long)0x8000000000000000ULL;
+  return (long long)v;
+}
+
+// math.Sin / math.Cos (Go sin.go, Cephes; |x| < 2^29, larger -> NaN here,
+// where Go would use Payne-Hanek: flagged by the caller as unpinned).
+__device__ __forceinline__ double go_trig(double x, bool want_cos) {
+  const double S0 = 1.58962301576546568060e-10, S1 = -2.50507477628578072866e-8, S2 = 2.75573136213857245213e-6,
+               S3 = -1.98412698295895385996e-4, S4 = 8.33333333332211858878e-3, S5 = -1.66666666666666307295e-1;
+  const double C0 = -1.13585365213876817300e-11, C1 = 2.08757008419747316778e-9, C2 = -2.75573141792967388112e-7,
+               C3 = 2.48015872888517045348e-5, C4 = -1.38888888888730564116e-3, C5 = 4.16666666666665929218e-2;
+  const double PI4A = 7.85398125648498535156e-1, PI4B = 3.77489470793079817668e-8, PI4C = 2.69515142907905952645e-15;
+  if (__builtin_isnan(x) || __builtin_isinf(x)) return __builtin_nan("");
+  if (!want_cos && x == 0) return x;
+  bool sign = false;
+  if (want_cos) {
+    x = __builtin_fabs(x);
+  } else if (x < 0) {
+    x = -x;
+    sign = true;
+  }
+  if (x >= 536870912.0) return __builtin_nan("");
+  unsigned long long j = (unsigned long long)(x * 1.2732395447351628);
+  double y = (double)j;
+  if (j & 1) {
+    j++;
+    y++;
+  }
+  j &= 7;
+  double z = ((x - y * PI4A) - y * PI4B) - y * PI4C;
+  if (j > 3) {
+    j -= 4;
+    sign = !sign;
+  }
+  if (want_cos && j > 1) sign = !sign;
+  double zz = z * z;
+  bool use_cos_poly = want_cos ? !(j == 1 || j == 2) : (j == 1 || j == 2);
+  if (use_cos_poly)
+    y = 1.0 - 0.5 * zz + zz * zz * ((((((C0 * zz) + C1) * zz + C2) * zz + C3) * zz + C4) * zz + C5);
+  else
+    y = z + z * zz * ((((((S0 * zz) + S1) * zz + S2) * zz + S3) * zz + S4) * zz + S5);
+  return sign ? -y : y;
+}
+__device__ __forceinline__ double go_sin(double x) { return go_trig(x, false); }
+__device__ __forceinline__ double go_cos(double x) { return go_trig(x, true); }
+
+// math.Atan / Asin / Acos / Atan2 (Go atan.go, asin.go, atan2.go).
+__device__ __forceinline__ double go_xatan(double x) {
+  const double P0 = -8.750608600031904122785e-01, P1 = -1.615753718733365076637e+01,
+               P2 = -7.500855792314704667340e+01, P3 = -1.228866684490136173410e+02,
+               P4 = -6.485021904942025371773e+01, Q0 = +2.485846490142306297962e+01,
+               Q1 = +1.650270098316988542046e+02, Q2 = +4.328810604912902668951e+02,
+               Q3 = +4.853903996359136964868e+02, Q4 = +1.945506571482613964425e+02;
+  double z = x * x;
+  z = z * ((((P0 * z + P1) * z + P2) * z + P3) * z + P4) / (((((z + Q0) * z + Q1) * z + Q2) * z + Q3) * z + Q4);
+  return x * z + x;
+}
+__device__ __forceinline__ double go_satan(double x) {
+  const double Morebits = 6.123233995736765886130e-17, Tan3pio8 = 2.41421356237309504880;
+  if (x <= 0.66) return go_xatan(x);
+  if (x > Tan3pio8) return 1.5707963267948966 - go_xatan(1 / x) + Morebits;
+  return 0.7853981633974483 + go_xatan((x - 1) / (x + 1)) + 0.5 * Morebits;
+}
+__device__ __forceinline__ double go_acos(double x) {
+  double a;  // Asin(x)
+  if (x == 0) {
+    a = x;
+  } else {
+    bool sign = x < 0;
+    double ax = sign ? -x : x;
+    if (ax > 1) return __builtin_nan("");
+    double temp = __builtin_sqrt(1 - ax * ax);
+    temp = (ax > 0.7) ? 1.5707963267948966 - go_satan(temp / ax) : go_satan(ax / temp);
+    a = sign ? -temp : temp;
+  }
+  return 1.5707963267948966 - a;
+}
+__device__ __forceinline__ double go_atan2(double y, double x) {
+  const double PI = 3.141592653589793;
+  if (__builtin_isnan(y) || __builtin_isnan(x)) return __builtin_nan("");
+  if (y == 0) {
+    if (x >= 0 && !signbit64(x)) return __builtin_copysign(0.0, y);
+    return __builtin_copysign(PI, y);
+  }
+  if (x == 0) return __builtin_copysign(1.5707963267948966, y);
+  if (__builtin_isinf(x)) {
+    if (x > 0) return __builtin_isinf(y) ? __builtin_copysign(0.7853981633974483, y) : __builtin_copysign(0.0, y);
+    return __builtin_isinf(y) ? __builtin_copysign(2.356194490192345, y) : __builtin_copysign(PI, y);
+  }
+  if (__builtin_isinf(y)) return __builtin_copysign(1.5707963267948966, y);
+  double r = y / x;
+  double q = (r == 0) ? r : (r > 0 ? go_satan(r) : -go_satan(-r));
+  if (x < 0) return q <= 0 ? q + PI : q - PI;
+  return q;
+}
+
 // uint32(v) for float64 v as Go compiles it on amd64 (CVTTSD2SQ, low 32 bits).
 __device__ __forceinline__ uint32_t go_f64_to_u32(double v) {
   if (!(v > -9223372036854775808.0 && v < 9223372036854775808.0)) return 0u;

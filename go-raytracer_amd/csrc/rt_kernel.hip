@@ -86,9 +86,9 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8 };
 // pend_d[3] kr packed. The CORE fields (Lw, kr, packed) of the first
 // RT_LDS_FRAMES levels live in LDS instead; cfirst/pending (only used when a
 // material is both reflective and transparent) always live in HBM.
-enum { FRAME_FIELDS = 14, CORE = 5 };
+enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
-enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_COUNT = 7, ST_PHASE = 16, N_PHASE = 8 };
+enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_SURFERR = 7, ST_COUNT = 8, ST_PHASE = 16, N_PHASE = 8 };
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
 #ifndef RT_LDS_MAX
 #define RT_LDS_MAX (40 * 1024)
@@ -97,7 +97,9 @@ enum { LDS_MAX_BYTES = RT_LDS_MAX };
 
 struct Params {
   int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
-  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, blob_bytes;
+  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_code, off_consts, off_entry, blob_bytes;
+  int lds_vm_off;     // LDS byte offset of the per-lane VM material records (LDS flavour)
+  double* vm_global;  // per-lane VM material records (global flavour)
   const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
   unsigned int* queue;
   unsigned long long* stats;
@@ -365,7 +367,113 @@ __device__ __forceinline__ d3 ld3(const double* f, int field) {
 __device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ? 12 : 13); }
 
 // Frame flags (packed with the material index).
-enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8 };
+enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16 };
+
+// ---------------------------------------------------------------------------
+// Closure-surface VM: executes a straight-line register
+// program compiled on the host from a GML surface function
+// (go-raytracer_amd/gml/surface_compiler.py) -- the device counterpart of
+// EvalSurfaceFn (evaluator.go:672-727). Registers are 64-bit (f64 / i64 /
+// bool); r0..r9 = Material, r10 = face, r11 = u, r12 = v. Go semantics:
+// int64 wraparound, truncating divi/modi, floor/frac via amd64 float->int,
+// Cephes sin/cos on degrees * (Pi/180). Returns true on a run-time error
+// (the reference would panic).
+// ---------------------------------------------------------------------------
+enum VmOp {
+  VM_NOP, VM_CONST, VM_MOV, VM_ADDF, VM_SUBF, VM_MULF, VM_DIVF, VM_NEGF, VM_ADDI, VM_SUBI, VM_MULI, VM_DIVI,
+  VM_MODI, VM_NEGI, VM_LTF, VM_EQF, VM_LTI, VM_EQI, VM_SEL, VM_FLOOR, VM_FRAC, VM_SQRT, VM_SIN, VM_COS,
+  VM_CLAMPF, VM_CLAMPI, VM_TBL, VM_AND, VM_OR, VM_NOT, VM_ERR, VM_RET
+};
+enum { VM_REGS = 64, VM_MAX_STEPS = 8192 };
+
+// Inlined: as an out-of-line call reading the LDS-staged program through
+// generic pointers it rendered wrong pixels on gfx950 (measured: the global
+// blob path and the inlined call are exact), and inlining needs less scratch.
+__device__ __forceinline__ bool run_vm(const uint32_t* code, const uint64_t* consts, int pc, long long face, double u,
+                                    double v, double* out) {
+  uint64_t R[VM_REGS];
+  R[10] = (uint64_t)face;
+  R[11] = (uint64_t)__double_as_longlong(u);
+  R[12] = (uint64_t)__double_as_longlong(v);
+  bool err = false;
+#define F_(r) __longlong_as_double((long long)R[r])
+#define I_(r) ((long long)R[r])
+#define SETF(x) R[d] = (uint64_t)__double_as_longlong(x)
+  for (int steps = 0; steps < VM_MAX_STEPS; steps++, pc += 2) {
+    const uint32_t w0 = code[pc], c = code[pc + 1];
+    const int op = (int)(w0 & 0xff), d = (int)((w0 >> 8) & 0x3f), a = (int)((w0 >> 16) & 0x3f),
+              b = (int)((w0 >> 24) & 0x3f);
+    switch (op) {
+      case VM_RET:
+        for (int k = 0; k < 10; k++) out[k] = F_(k);
+        return err;
+      case VM_CONST: R[d] = consts[c]; break;
+      case VM_MOV: R[d] = R[a]; break;
+      case VM_ADDF: SETF(F_(a) + F_(b)); break;
+      case VM_SUBF: SETF(F_(a) - F_(b)); break;
+      case VM_MULF: SETF(F_(a) * F_(b)); break;
+      case VM_DIVF: SETF(F_(a) / F_(b)); break;
+      case VM_NEGF: SETF(-F_(a)); break;
+      case VM_ADDI: R[d] = R[a] + R[b]; break;
+      case VM_SUBI: R[d] = R[a] - R[b]; break;
+      case VM_MULI: R[d] = R[a] * R[b]; break;
+      case VM_DIVI: {  // Go: truncating; MinInt64 / -1 wraps; /0 is checked by ERR
+        long long x = I_(a), y = I_(b);
+        R[d] = y == 0 ? 0 : (y == -1 ? (uint64_t)0 - (uint64_t)x : (uint64_t)(x / y));
+        break;
+      }
+      case VM_MODI: {
+        long long x = I_(a), y = I_(b);
+        R[d] = (y == 0 || y == -1) ? 0 : (uint64_t)(x % y);
+        break;
+      }
+      case VM_NEGI: R[d] = (uint64_t)0 - R[a]; break;
+      case VM_LTF: R[d] = F_(a) < F_(b); break;
+      case VM_EQF: R[d] = F_(a) == F_(b); break;
+      case VM_LTI: R[d] = I_(a) < I_(b); break;
+      case VM_EQI: R[d] = R[a] == R[b]; break;
+      case VM_SEL: R[d] = R[a] ? R[b] : R[c & 0x3f]; break;
+      case VM_FLOOR: {
+        double x = F_(a);
+        R[d] = (uint64_t)go_f2i(__builtin_isfinite(x) ? __builtin_floor(x) : x);
+        break;
+      }
+      case VM_FRAC: {
+        double x = F_(a);
+        SETF(x - (double)go_f2i(x));
+        break;
+      }
+      case VM_SQRT: SETF(__builtin_sqrt(F_(a))); break;
+      case VM_SIN: SETF(go_sin(0.017453292519943295 * F_(a))); break;
+      case VM_COS: SETF(go_cos(0.017453292519943295 * F_(a))); break;
+      case VM_CLAMPF: {
+        double x = F_(a);
+        SETF(x < 0 ? 0.0 : (x > 1 ? 1.0 : x));
+        break;
+      }
+      case VM_CLAMPI: {
+        long long x = I_(a);
+        R[d] = (uint64_t)(x < 0 ? 0 : (x > 1 ? 1 : x));
+        break;
+      }
+      case VM_TBL: {  // consts[c] = n, then n entries; bounds are checked by ERR
+        long long n = (long long)consts[c], i = I_(a);
+        i = i < 0 ? 0 : (i >= n ? n - 1 : i);
+        R[d] = consts[c + 1 + i];
+        break;
+      }
+      case VM_AND: R[d] = (R[a] != 0) && (R[b] != 0); break;
+      case VM_OR: R[d] = (R[a] != 0) || (R[b] != 0); break;
+      case VM_NOT: R[d] = R[a] == 0; break;
+      case VM_ERR: err = err || (R[a] != 0); break;
+      default: return true;
+    }
+  }
+#undef F_
+#undef I_
+#undef SETF
+  return true;  // malformed program (no RET)
+}
 
 // traceRay's final combine (raytracer.go:557-561).
 __device__ __forceinline__ d3 combine(bool tmode, d3 lw, d3 col, double refl, double kr, d3 R, d3 Tr) {
@@ -374,6 +482,9 @@ __device__ __forceinline__ d3 combine(bool tmode, d3 lw, d3 col, double refl, do
 }
 
 struct View {
+  const int* entry;
+  const uint32_t* code;
+  const uint64_t* consts;
   const double* geo;
   const double* shade;
   const double* mats;
@@ -406,6 +517,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   S.lights = reinterpret_cast<const double*>(base + P.off_lights);
   S.kind = reinterpret_cast<const int*>(base + P.off_kind);
   S.objmat = reinterpret_cast<const int*>(base + P.off_objmat);
+  S.code = reinterpret_cast<const uint32_t*>(base + P.off_code);
+  S.entry = reinterpret_cast<const int*>(base + P.off_entry);
+  S.consts = reinterpret_cast<const uint64_t*>(base + P.off_consts);
 
   const int lane = (int)(threadIdx.x & 63);
   const int wslot = (int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
@@ -423,6 +537,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     else
       frame_ptr(stk, level)[core_gfield(c) * 64] = v;
   };
+  // Per-lane material record written by the surface VM (same layout as mats).
+  double* vmrec;
+  if constexpr (LDS)
+    vmrec = reinterpret_cast<double*>(smem + P.lds_vm_off) + (size_t)threadIdx.x * MAT;
+  else
+    vmrec = P.vm_global + ((size_t)wslot * 64 + lane) * MAT;
   const d3 eye = mk(0.0, 0.0, -1.0);  // raytracer.go:605-609
 
   // lane state
@@ -441,7 +561,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // wave-uniform pool and counters
   unsigned int pool_next = 0, pool_end = 0;
   bool exhausted = false;
-  uint64_t c_shadow = 0, c_traced = 0, c_shaded = 0;
+  uint64_t c_shadow = 0, c_traced = 0, c_shaded = 0, c_surferr = 0;
   uint64_t c_stest[4] = {0, 0, 0, 0};
 #ifdef RT_PHASE_TIMING
   uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -517,7 +637,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               lw = mk(core_ld(sp - 1, 0), core_ld(sp - 1, 1), core_ld(sp - 1, 2));
               kr = core_ld(sp - 1, 3);
             }
-            res = combine((fl & FL_TMODE) != 0, lw, mk(FM[0], FM[1], FM[2]), FM[3], kr, R, Tr);
+            d3 fcol;
+            double frefl;
+            if (fl & FL_VMMAT) {
+              fcol = ld3(f, 14);
+              frefl = f[17 * 64];
+            } else {
+              fcol = mk(FM[0], FM[1], FM[2]);
+              frefl = FM[3];
+            }
+            res = combine((fl & FL_TMODE) != 0, lw, fcol, frefl, kr, R, Tr);
             sp--;
           }
           pf_valid = false;
@@ -659,6 +788,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     // ComputeSurfaceProps (raytracer.go:106-122, 182-194, 242-260, 339-370)
     d3 pw = mk(0, 0, 0), nw = mk(0, 0, 1);
     int mat = 0;
+    bool surf_bad = false;
     if (hit) {
       const double* g = S.geo + (size_t)hit_i * GEO;
       const double* s = S.shade + (size_t)hit_i * SHD;
@@ -678,11 +808,53 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         nw = mk(s[12 + hit_f * 3], s[13 + hit_f * 3], s[14 + hit_f * 3]);
       }
       mat = S.objmat[(size_t)hit_i * OMAT + hit_f];
+      if (mat < 0) {
+        // Closure surface: (face, u, v) as ComputeSurfaceProps computes them
+        // (raytracer.go:124-150, 196-205, 249, 339-359), then the VM.
+        double u, v;
+        bool bad = false;
+        long long face = (k == RT_PLANE) ? 0 : hit_f;
+        if (k == RT_SPHERE) {
+          bad = __builtin_fabs(p.y) > 1;
+          v = (p.y + 1.0) / 2.0;
+          u = go_acos(p.z / __builtin_sqrt(1.0 - p.y * p.y)) / 6.283185307179586;
+        } else if (k == RT_CYLINDER && hit_f == 0) {
+          u = (go_atan2(p.x, p.z) + 3.141592653589793) / 6.283185307179586;
+          v = p.y;
+        } else {
+          u = p.x;
+          v = p.z;
+        }
+        double r[10];
+        bad = run_vm(S.code, S.consts, S.entry[-mat - 1], face, u, v, r) || bad;
+        if (bad)  // counted; the material reads as all-zero (oracle convention)
+          for (int k = 0; k < 10; k++) r[k] = 0.0;
+        vmrec[0] = r[0];
+        vmrec[1] = r[1];
+        vmrec[2] = r[2];
+        vmrec[3] = r[3];
+        const double fz = r[4];
+        if (fz >= 0) {  // baked constant fuzz offset (raytracer.go:516-522)
+          const double cf = go_cos(fz), sf = go_sin(fz);
+          vmrec[4] = fz * cf * cf;
+          vmrec[5] = fz * sf * sf;
+          vmrec[6] = 1.0;
+        } else {
+          vmrec[4] = vmrec[5] = vmrec[6] = 0.0;
+        }
+        vmrec[7] = r[5];
+        vmrec[8] = r[6];
+        vmrec[9] = r[7];
+        vmrec[10] = r[8];
+        vmrec[11] = r[9];
+        surf_bad = bad;
+      }
     }
+    c_surferr += popc_ballot(surf_bad);
 
     // computeLighting + inShadow (raytracer.go:372-429)
     PH_MARK(3);
-    const double* M = S.mats + (size_t)mat * MAT;
+    const double* M = mat >= 0 ? S.mats + (size_t)mat * MAT : vmrec;
     d3 L = mk(0, 0, 0);
     if (hit) L = scale(mk(P.amb[0], P.amb[1], P.amb[2]), M[9]);
     const double rlen = len(ray.d);
@@ -802,8 +974,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             st3(f, 9, trr.d);
           }
           core_st(sp, 3, kr);
-          long long packed =
-              ((long long)mat << 8) | (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
+          if (mat < 0) {  // the VM record is per lane: keep what the combine needs
+            double* f = frame_ptr(stk, sp);
+            st3(f, 14, col);
+            f[17 * 64] = refl;
+          }
+          long long packed = ((long long)(mat < 0 ? 0 : mat) << 8) | (mat < 0 ? FL_VMMAT : 0) |
+                             (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
           core_st(sp, 4, __longlong_as_double(packed));
           sp++;
           ray = hasR ? rr : trr;
@@ -826,8 +1003,21 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     atomicAdd(P.stats + ST_TRACED, (unsigned long long)c_traced);
     atomicAdd(P.stats + ST_SHADOW, (unsigned long long)c_shadow);
     atomicAdd(P.stats + ST_SHADED, (unsigned long long)c_shaded);
+    atomicAdd(P.stats + ST_SURFERR, (unsigned long long)c_surferr);
     for (int k = 0; k < 4; k++) atomicAdd(P.stats + ST_STESTS + k, (unsigned long long)c_stest[k]);
   }
+}
+
+// Diagnostic: run surface program `prog` of the current scene on n inputs.
+__global__ void rt_debug_vm_kernel(const char* __restrict__ blob, int off_code, int off_consts, int off_entry, int prog,
+                                   const long long* face, const double* u, const double* v, double* out, int* err,
+                                   int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + off_code);
+  const uint64_t* consts = reinterpret_cast<const uint64_t*>(blob + off_consts);
+  const int* entry = reinterpret_cast<const int*>(blob + off_entry);
+  err[i] = run_vm(code, consts, entry[prog], face[i], u[i], v[i], out + (size_t)i * 10) ? 1 : 0;
 }
 
 template __global__ void rt_render_kernel<true>(const char* __restrict__, Params);
@@ -989,6 +1179,7 @@ struct DevScene {
   int blob_bytes = 0;
   int off_geo = 0, off_shade = 0, off_mats = 0, off_lights = 0, off_kind = 0, off_objmat = 0;
   std::vector<int> kinds;  // host copy for the per-kind test counts
+  int off_code = 0, off_consts = 0, off_entry = 0, num_programs = 0;
 };
 
 int align16(int v) { return (v + 15) & ~15; }
@@ -1005,6 +1196,8 @@ struct rt_context {
   unsigned int* queue = nullptr;
   unsigned long long* stats = nullptr;
   double* stack = nullptr;
+  double* vm_global = nullptr;  // per-lane VM material records (global flavour)
+  size_t vm_global_bytes = 0;
   size_t stack_bytes = 0;
   int stack_waves = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1117,6 +1310,7 @@ void rt_destroy(rt_context* c) {
   (void)hipFree(c->queue);
   (void)hipFree(c->stats);
   (void)hipFree(c->stack);
+  (void)hipFree(c->vm_global);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -1156,8 +1350,8 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     if (o.kind < 0 || o.kind >= RT_NUM_KINDS) return fail(RT_E_INVALID, "unknown scene object type");
     kind[i] = o.kind;
     for (int f = 0; f < RT_MAX_FACES; f++) {
-      if (o.material[f] < 0 || o.material[f] >= in->num_materials)
-        return fail(RT_E_INVALID, "material index out of range");
+      if (o.material[f] >= in->num_materials || o.material[f] < -std::max(0, in->num_programs))
+        return fail(RT_E_INVALID, "material / surface program index out of range");
       objmat[(size_t)i * OMAT + f] = o.material[f];
     }
     M4 o2w = ident(), w2o = ident();  // raytracer.go:757-762
@@ -1245,7 +1439,43 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   s.off_lights = align16(s.off_mats + (int)(mats.size() * sizeof(double)));
   s.off_kind = align16(s.off_lights + (int)(lights.size() * sizeof(double)));
   s.off_objmat = align16(s.off_kind + (int)(kind.size() * sizeof(int)));
-  s.blob_bytes = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
+  // Surface programs: validated so the device never reads outside them.
+  const int nprog = std::max(0, in->num_programs);
+  const int ncode = nprog ? in->program_code_words : 0, nconst = nprog ? in->program_const_count : 0;
+  if (nprog) {
+    if (!in->program_code || !in->program_consts || !in->program_entry || ncode <= 0 || nconst < 0)
+      return fail(RT_E_INVALID, "surface programs: NULL array or empty code");
+    for (int pi = 0; pi < nprog; pi++) {
+      int pc = in->program_entry[pi];
+      if (pc < 0 || (pc & 1)) return fail(RT_E_INVALID, "surface program entry out of range");
+      bool ret = false;
+      for (int steps = 0; steps < VM_MAX_STEPS && pc + 1 < ncode; steps++, pc += 2) {
+        uint32_t w0 = in->program_code[pc], cc = in->program_code[pc + 1];
+        int op = (int)(w0 & 0xff);
+        if (op > VM_RET || ((w0 >> 8) & 0xff) >= VM_REGS || ((w0 >> 16) & 0xff) >= VM_REGS ||
+            (w0 >> 24) >= VM_REGS)
+          return fail(RT_E_INVALID, "surface program: bad opcode or register");
+        if (op == VM_CONST && cc >= (uint32_t)nconst) return fail(RT_E_INVALID, "surface program: bad constant");
+        if (op == VM_TBL) {
+          if (cc >= (uint32_t)nconst) return fail(RT_E_INVALID, "surface program: bad table");
+          uint64_t n = in->program_consts[cc];
+          if (n == 0 || n > (uint64_t)nconst || cc + 1 + n > (uint64_t)nconst)
+            return fail(RT_E_INVALID, "surface program: bad table length");
+        }
+        if (op == VM_SEL && cc >= VM_REGS) return fail(RT_E_INVALID, "surface program: bad register");
+        if (op == VM_RET) {
+          ret = true;
+          break;
+        }
+      }
+      if (!ret) return fail(RT_E_INVALID, "surface program does not end in RET");
+    }
+  }
+  s.num_programs = nprog;
+  s.off_code = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
+  s.off_consts = align16(s.off_code + ncode * (int)sizeof(uint32_t));
+  s.off_entry = align16(s.off_consts + nconst * (int)sizeof(uint64_t));
+  s.blob_bytes = align16(s.off_entry + nprog * (int)sizeof(int));
   {
     std::vector<char> blob((size_t)s.blob_bytes, 0);
     std::memcpy(blob.data() + s.off_geo, geo.data(), geo.size() * sizeof(double));
@@ -1254,6 +1484,11 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     std::memcpy(blob.data() + s.off_lights, lights.data(), lights.size() * sizeof(double));
     std::memcpy(blob.data() + s.off_kind, kind.data(), kind.size() * sizeof(int));
     std::memcpy(blob.data() + s.off_objmat, objmat.data(), objmat.size() * sizeof(int));
+    if (nprog) {
+      std::memcpy(blob.data() + s.off_code, in->program_code, (size_t)ncode * sizeof(uint32_t));
+      std::memcpy(blob.data() + s.off_consts, in->program_consts, (size_t)nconst * sizeof(uint64_t));
+      std::memcpy(blob.data() + s.off_entry, in->program_entry, (size_t)nprog * sizeof(int));
+    }
     int rc = upload(&s.blob, blob);
     if (rc != RT_OK) {
       free_scene(s);
@@ -1276,6 +1511,19 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     c->stack_bytes = need;
   }
   c->stack_waves = (int)(c->stack_bytes / ((size_t)frames * FRAME_FIELDS * 64 * sizeof(double)));
+  if (nprog) {  // per-lane VM material records for the global-scene flavour
+    size_t vneed = (size_t)c->stack_waves * 64 * MAT * sizeof(double);
+    if (vneed > c->vm_global_bytes) {
+      (void)hipFree(c->vm_global);
+      c->vm_global = nullptr;
+      c->vm_global_bytes = 0;
+      if (hipMalloc((void**)&c->vm_global, vneed) != hipSuccess) {
+        free_scene(s);
+        return fail(RT_E_NOMEM, "surface VM record allocation failed");
+      }
+      c->vm_global_bytes = vneed;
+    }
+  }
   free_scene(c->sc);
   c->sc = s;
   c->has_scene = true;
@@ -1290,7 +1538,8 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   hipStream_t st = (hipStream_t)stream;
   const bool lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
   const int frames_off = lds ? s.blob_bytes : 0;
-  const int shmem = frames_off + WAVES_PER_WG * RT_LDS_FRAMES * CORE * 64 * (int)sizeof(double);
+  const int vm_off = frames_off + WAVES_PER_WG * RT_LDS_FRAMES * CORE * 64 * (int)sizeof(double);
+  const int shmem = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
   int per_cu = 0;
   if (lds) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, WG, shmem) != hipSuccess)
@@ -1311,6 +1560,11 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.off_lights = s.off_lights;
   P.off_kind = s.off_kind;
   P.off_objmat = s.off_objmat;
+  P.off_code = s.off_code;
+  P.off_consts = s.off_consts;
+  P.off_entry = s.off_entry;
+  P.lds_vm_off = vm_off;
+  P.vm_global = c->vm_global;
   P.blob_bytes = s.blob_bytes;
   P.jump = c->jump;
   P.queue = c->queue;
@@ -1397,6 +1651,7 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
     out->shadow_tests[k] = h[ST_STESTS + k];
   }
   out->shaded_hits = h[ST_SHADED];
+  out->surface_errors = h[ST_SURFERR];
 #ifdef RT_PHASE_TIMING
   {
     unsigned long long ph[N_PHASE];
@@ -1431,6 +1686,42 @@ int rt_last_kernel_ms(rt_context* c, double* ms_out) {
   HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   *ms_out = ms;
   return RT_OK;
+}
+
+int rt_debug_run_surface(rt_context* c, int program, int n, const long long* face, const double* u,
+                         const double* v, double* out10, int* err) {
+  if (!c || !c->has_scene || n <= 0 || !face || !u || !v || !out10 || !err)
+    return fail(RT_E_INVALID, "rt_debug_run_surface: bad arguments");
+  if (program < 0 || program >= c->sc.num_programs) return fail(RT_E_INVALID, "rt_debug_run_surface: no such program");
+  DeviceGuard guard(c->device);
+  long long* df = nullptr;
+  double *du = nullptr, *dv = nullptr, *dout = nullptr;
+  int* derr = nullptr;
+  int rc = RT_OK;
+  if (hipMalloc((void**)&df, n * sizeof(long long)) != hipSuccess || hipMalloc((void**)&du, n * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&dv, n * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&dout, (size_t)n * 10 * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&derr, n * sizeof(int)) != hipSuccess)
+    rc = fail(RT_E_NOMEM, "rt_debug_run_surface: alloc");
+  if (rc == RT_OK && (hipMemcpy(df, face, n * sizeof(long long), hipMemcpyHostToDevice) != hipSuccess ||
+                      hipMemcpy(du, u, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+                      hipMemcpy(dv, v, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
+    rc = fail(RT_E_DEVICE, "rt_debug_run_surface: copy");
+  if (rc == RT_OK) {
+    hipLaunchKernelGGL(rt_debug_vm_kernel, dim3((n + 63) / 64), dim3(64), 0, nullptr, (const char*)c->sc.blob,
+                       c->sc.off_code, c->sc.off_consts, c->sc.off_entry, program, df, du, dv, dout, derr, n);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      rc = fail(RT_E_DEVICE, "rt_debug_run_surface: launch");
+  }
+  if (rc == RT_OK && (hipMemcpy(out10, dout, (size_t)n * 10 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+                      hipMemcpy(err, derr, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess))
+    rc = fail(RT_E_DEVICE, "rt_debug_run_surface: copy back");
+  (void)hipFree(df);
+  (void)hipFree(du);
+  (void)hipFree(dv);
+  (void)hipFree(dout);
+  (void)hipFree(derr);
+  return rc;
 }
 
 int rt_render(const rt_scene* scene, uint8_t* rgba_out, rt_stats* stats) {

@@ -7,17 +7,26 @@ from .printer import render_args_lines  # noqa: F401
 from .syntax import ParseError  # noqa: F401
 
 
+def _hook(out):
+    def render(e, args):
+        # ConvertRenderArgsToScene clones the state for the render threads
+        # (raytracer.go:738-751); closure surfaces evaluate on that clone.
+        args.state = e.clone()
+        out.append((args, e))
+    return render
+
+
 def run_file(path):
-    """Evaluate a .gml file; returns the list of RenderArgs it rendered (in order)
-    and the final EvalState."""
+    """Evaluate a .gml file; returns the list of (RenderArgs, EvalState) it
+    rendered (in order) and the final EvalState."""
     out = []
-    st = EvalState(render=lambda e, a: out.append((a, e)))
+    st = EvalState(render=_hook(out))
     st.parse_and_eval_file(path)
     return out, st
 
 
 def run_text(text):
     out = []
-    st = EvalState(render=lambda e, a: out.append((a, e)))
+    st = EvalState(render=_hook(out))
     st.parse_and_eval(text)
     return out, st

@@ -22,11 +22,13 @@ class RenderError(RuntimeError):
     pass
 
 
-def load_library(path=LIB_PATH):
-    """Load librtamd.so and declare the include/rt_abi.h signatures."""
+def load_library(path=None):
+    """Load librtamd.so and declare the include/rt_abi.h signatures.
+    RT_AMD_LIB overrides the in-tree path (A/B builds of the same ABI)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("RT_AMD_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RenderError("HIP renderer library not built: %s (run __graft_entry__.build())" % path)
     l = C.CDLL(path)
@@ -49,6 +51,8 @@ def load_library(path=LIB_PATH):
     l.rt_read_stats.restype = i
     l.rt_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
     l.rt_last_kernel_ms.restype = i
+    l.rt_debug_run_surface.argtypes = [vp, i, i, vp, vp, vp, vp, vp]
+    l.rt_debug_run_surface.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
     l.rt_render.restype = i
     if l.rt_abi_version() != 1:
@@ -134,6 +138,18 @@ class RenderContext:
         ms = C.c_double()
         _check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)), "rt_last_kernel_ms")
         return ms.value
+
+    def debug_run_surface(self, program, face, u, v):
+        """Diagnostic: run one surface program on the device for arrays of inputs."""
+        face = np.ascontiguousarray(face, dtype=np.int64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        n = len(face)
+        out = np.zeros((n, 10), dtype=np.float64)
+        err = np.zeros(n, dtype=np.int32)
+        _check(self.lib.rt_debug_run_surface(self.handle, int(program), n, face.ctypes.data, u.ctypes.data,
+                                             v.ctypes.data, out.ctypes.data, err.ctypes.data), "rt_debug_run_surface")
+        return out, err
 
     def render(self, y0=0, y1=None):
         """Synchronous render of rows [y0, y1) -> numpy uint8 [rows, W, 4]."""

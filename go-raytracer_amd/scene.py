@@ -152,6 +152,9 @@ class RenderArgs:
     file: str = "out.ppm"
     bg_start: tuple = (0.0, 0.0, 0.0)
     bg_end: tuple = (0.0, 0.0, 0.0)
+    # GML EvalState at the render call (per-frame clone, raytracer.go:738-751):
+    # closure surfaces evaluate on its stack. None for scenes built in Python.
+    state: object = None
 
 
 _NFACES = {abi.RT_SPHERE: 1, abi.RT_PLANE: 1, abi.RT_CUBE: 6, abi.RT_CYLINDER: 3}
@@ -201,13 +204,25 @@ def convert(args: RenderArgs) -> abi.PackedScene:
             mats.append(m)
         return mat_index[m]
 
+    programs = []     # (SurfaceFn, Program)
+    prog_index = {}
+
+    def pidx(sf):
+        key = id(sf.closure)
+        if key not in prog_index:
+            from .gml.surface_compiler import compile_surface
+            stack = args.state.stack if args.state is not None else ()
+            prog_index[key] = len(programs)
+            programs.append((sf, compile_surface(sf, stack)))
+        return -(prog_index[key] + 1)
+
     c_objs = (abi.rt_object * max(1, len(objs)))()
     for i, o in enumerate(objs):
         kind = _KIND[type(o)]
         co = c_objs[i]
         co.kind = kind
         fm = _face_materials(o, kind)
-        idx = [midx(m) for m in fm]
+        idx = [midx(m) if isinstance(m, Material) else pidx(m) for m in fm]
         for f in range(abi.RT_MAX_FACES):
             co.material[f] = idx[f] if f < len(idx) else idx[0]
         if o.transform_mat is not None:
@@ -255,4 +270,27 @@ def convert(args: RenderArgs) -> abi.PackedScene:
     sc.materials = C.cast(c_mats, C.POINTER(abi.rt_material))
     sc.num_objects = len(objs)
     sc.num_materials = len(mats)
-    return abi.PackedScene(sc, c_lights, c_objs, c_mats)
+    packed_progs = None
+    if programs:
+        from .gml.surface_compiler import OP
+        words, consts, entry = [], [], []
+        for sf, prog in programs:
+            base = len(consts)
+            entry.append(len(words))
+            for op, d, a, b, c in prog.code:
+                if op in (OP["CONST"], OP["TBL"]):
+                    c += base
+                words.append(op | (d << 8) | (a << 16) | (b << 24))
+                words.append(c & 0xFFFFFFFF)
+            consts.extend(prog.consts)
+        c_code = (C.c_uint32 * len(words))(*words)
+        c_consts = (C.c_uint64 * max(1, len(consts)))(*consts)
+        c_entry = (C.c_int32 * len(entry))(*entry)
+        sc.program_code = C.cast(c_code, C.POINTER(C.c_uint32))
+        sc.program_consts = C.cast(c_consts, C.POINTER(C.c_uint64))
+        sc.program_entry = C.cast(c_entry, C.POINTER(C.c_int32))
+        sc.num_programs = len(programs)
+        sc.program_code_words = len(words)
+        sc.program_const_count = len(consts)
+        packed_progs = (c_code, c_consts, c_entry, [sf for sf, _ in programs], args.state)
+    return abi.PackedScene(sc, c_lights, c_objs, c_mats, packed_progs)

@@ -83,6 +83,13 @@ typedef struct rt_point_light {
  *   plane_point,
  *   plane_normal   RT_PLANE only: gml.Plane.Plane (evaluator.go:813-821 builds
  *                  point (0,0,0), normal (0,1,0)). */
+/* Closure surfaces (GML surface functions that depend on face/u/v) run on the
+ * device as straight-line register programs compiled by the host
+ * (go-raytracer_amd/gml/surface_compiler.py). A face whose material index is
+ * negative uses program (-material[f] - 1): it receives face (i64), u, v (f64)
+ * as computed by the reference's ComputeSurfaceProps (raytracer.go:124-150,
+ * 196-205, 339-359) and yields the 10 gml.Material fields, exactly what
+ * EvalSurfaceFn (evaluator.go:672-727) returns for that hit. */
 typedef struct rt_object {
     int32_t kind;
     int32_t has_transform;
@@ -109,6 +116,16 @@ typedef struct rt_scene {
     const rt_material *materials;
     int32_t num_objects;
     int32_t num_materials;
+    /* surface programs (may be empty): instruction words of all programs,
+     * each 2 x uint32 (w0 = op | dst<<8 | a<<16 | b<<24, w1 = c); entry word
+     * offset per program; one shared constant pool of 64-bit patterns. */
+    const uint32_t *program_code;
+    const uint64_t *program_consts;
+    const int32_t *program_entry;
+    int32_t num_programs;
+    int32_t program_code_words;
+    int32_t program_const_count;
+    int32_t reserved0;
 } rt_scene;
 
 /* Work counters, identical in the CPU oracle and the GPU path.
@@ -119,7 +136,8 @@ typedef struct rt_scene {
  *                    (raytracer.go:383)
  *   tests[k]         Intersect calls on kind k made by closestHit
  *   shadow_tests[k]  Intersect calls on kind k made by inShadow (early exit)
- *   shaded_hits      ComputeSurfaceProps + computeLighting evaluations */
+ *   shaded_hits      ComputeSurfaceProps + computeLighting evaluations
+ *   surface_errors   closure-surface evaluations that raised an error */
 typedef struct rt_stats {
     uint64_t primary_rays;
     uint64_t secondary_rays;
@@ -127,6 +145,9 @@ typedef struct rt_stats {
     uint64_t tests[RT_NUM_KINDS];
     uint64_t shadow_tests[RT_NUM_KINDS];
     uint64_t shaded_hits;
+    uint64_t surface_errors; /* hits whose surface evaluation failed; the
+                              * reference panics on the first one
+                              * (raytracer.go:499-501) */
     double kernel_ms;    /* device time of the last render (GPU path)  */
 } rt_stats;
 
@@ -174,6 +195,12 @@ int rt_read_stats(rt_context *ctx, void *stream, int reset, rt_stats *out);
 /* Device time (ms) of the most recent rt_render_rows_async on this context,
  * measured with HIP events on the stream it was launched on. Synchronises. */
 int rt_last_kernel_ms(rt_context *ctx, double *ms_out);
+
+/* Diagnostic (tests): run surface program `program` of the context's scene on
+ * n (face, u, v) inputs on the device; out10 receives n x 10 Material fields
+ * (rt_material order), err n flags (1 = the reference would raise). */
+int rt_debug_run_surface(rt_context *ctx, int program, int n, const long long *face,
+                         const double *u, const double *v, double *out10, int *err);
 
 /* Convenience, synchronous whole-frame Render() into host memory
  * (width*height*4 bytes, caller-owned). Uses a cached context on the

@@ -220,6 +220,64 @@ static inline double go_tan(double x) {
     return sign ? -y : y;
 }
 
+/* math.Atan / Asin / Acos / Atan2 (atan.go, asin.go, atan2.go): Cephes
+ * rational approximation with argument reduction. Used for closure-surface
+ * u coordinates (raytracer.go:147, :345). */
+#define GO_PI_2 1.5707963267948966  /* const Pi/2 */
+#define GO_PI_4 0.7853981633974483  /* const Pi/4 */
+static inline double go_xatan(double x) {
+    const double P0 = -8.750608600031904122785e-01, P1 = -1.615753718733365076637e+01,
+                 P2 = -7.500855792314704667340e+01, P3 = -1.228866684490136173410e+02,
+                 P4 = -6.485021904942025371773e+01, Q0 = +2.485846490142306297962e+01,
+                 Q1 = +1.650270098316988542046e+02, Q2 = +4.328810604912902668951e+02,
+                 Q3 = +4.853903996359136964868e+02, Q4 = +1.945506571482613964425e+02;
+    double z = x * x;
+    z = z * ((((P0 * z + P1) * z + P2) * z + P3) * z + P4) / (((((z + Q0) * z + Q1) * z + Q2) * z + Q3) * z + Q4);
+    z = x * z + x;
+    return z;
+}
+static inline double go_satan(double x) {
+    const double Morebits = 6.123233995736765886130e-17, Tan3pio8 = 2.41421356237309504880;
+    if (x <= 0.66) return go_xatan(x);
+    if (x > Tan3pio8) return GO_PI_2 - go_xatan(1 / x) + Morebits;
+    return GO_PI_4 + go_xatan((x - 1) / (x + 1)) + 0.5 * Morebits;
+}
+static inline double go_atan(double x) {
+    if (x == 0) return x;
+    if (x > 0) return go_satan(x);
+    return -go_satan(-x);
+}
+static inline double go_asin(double x) {
+    if (x == 0) return x;
+    int sign = 0;
+    if (x < 0) { x = -x; sign = 1; }
+    if (x > 1) return NAN;
+    double temp = sqrt(1 - x * x);
+    if (x > 0.7) temp = GO_PI_2 - go_satan(temp / x);
+    else temp = go_satan(x / temp);
+    return sign ? -temp : temp;
+}
+static inline double go_acos(double x) { return GO_PI_2 - go_asin(x); }
+static inline double go_atan2(double y, double x) {
+    if (isnan(y) || isnan(x)) return NAN;
+    if (y == 0) {
+        if (x >= 0 && !go_signbit(x)) return copysign(0, y);
+        return copysign(M_PI, y);
+    }
+    if (x == 0) return copysign(GO_PI_2, y);
+    if (isinf(x)) {
+        if (x > 0) return isinf(y) ? copysign(GO_PI_4, y) : copysign(0, y);
+        return isinf(y) ? copysign(2.356194490192345, y) : copysign(M_PI, y);
+    }
+    if (isinf(y)) return copysign(GO_PI_2, y);
+    double q = go_atan(y / x);
+    if (x < 0) {
+        if (q <= 0) return q + M_PI;
+        return q - M_PI;
+    }
+    return q;
+}
+
 /* math/rand/v2 PCG (pcg.go): state = state*mul + inc mod 2^128; DXSM. */
 typedef struct go_pcg { uint64_t hi, lo; } go_pcg;
 

@@ -235,7 +235,16 @@ static int object_intersect(const object *o, ray r, double *t, vec3 *p, int *fac
 }
 
 /* ---- per-thread counters ------------------------------------------------ */
-typedef struct { uint64_t secondary, shadow, tests[4], shadow_tests[4], shaded; } counters;
+typedef struct { uint64_t secondary, shadow, tests[4], shadow_tests[4], shaded, surface_errors; } counters;
+
+/* Closure surfaces: faces with a negative material index are evaluated by a
+ * host callback that runs the GML interpreter (EvalSurfaceFn,
+ * evaluator.go:672-727) on (face, u, v). Returns 0 on success and fills the
+ * 10 gml.Material fields (rt_material order). */
+typedef int (*oracle_surface_cb)(int program, int face, double u, double v, double *out10);
+static oracle_surface_cb g_surface_cb = NULL;
+static pthread_mutex_t g_cb_lock = PTHREAD_MUTEX_INITIALIZER;
+void oracle_set_surface_callback(oracle_surface_cb cb) { g_surface_cb = cb; }
 
 static int closest_hit(const scene *s, ray r, hit *h, counters *cnt) {          /* :469-483 */
     int found = 0;
@@ -248,9 +257,29 @@ static int closest_hit(const scene *s, ray r, hit *h, counters *cnt) {          
     return found;
 }
 
-typedef struct { vec3 pw, nw; const rt_material *mat; } hitex;                  /* :31-36 */
+typedef struct { vec3 pw, nw; const rt_material *mat; rt_material own; } hitex; /* :31-36 */
 
-static void surface_props(const scene *s, const hit *h, hitex *x) {
+static void eval_program(int prog, int face, double u, double v, int bad, hitex *x, counters *cnt) {
+    double out[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int rc = bad;
+    if (!bad) {
+        pthread_mutex_lock(&g_cb_lock);
+        rc = g_surface_cb ? g_surface_cb(prog, face, u, v, out) : -1;
+        pthread_mutex_unlock(&g_cb_lock);
+    }
+    if (rc != 0) { cnt->surface_errors++; memset(out, 0, sizeof out); }
+    memcpy(x->own.color, out, 3 * sizeof(double));
+    x->own.reflectivity = out[3];
+    x->own.fuzziness = out[4];
+    x->own.transparency = out[5];
+    x->own.refractive_index = out[6];
+    x->own.kd = out[7];
+    x->own.ks = out[8];
+    x->own.specular_exponent = out[9];
+    x->mat = &x->own;
+}
+
+static void surface_props(const scene *s, const hit *h, hitex *x, counters *cnt) {
     const object *o = &s->obj[h->obj];
     switch (o->kind) {
     case RT_SPHERE:                                                             /* :106-122 */
@@ -275,7 +304,36 @@ static void surface_props(const scene *s, const hit *h, hitex *x) {
         break;
     }
     }
-    x->mat = &s->mats[o->material[h->face]];
+    int mi = o->material[h->face];
+    if (mi >= 0) {
+        x->mat = &s->mats[mi];
+        return;
+    }
+    /* closure surface: u, v as ComputeSurfaceProps computes them */
+    double u = 0, v = 0;
+    int bad = 0;
+    switch (o->kind) {
+    case RT_SPHERE:                                                             /* :124-150 */
+        if (fabs(h->p.y) > 1) bad = 1;
+        v = (h->p.y + 1.0) / 2.0;
+        u = go_acos(h->p.z / sqrt(1.0 - h->p.y * h->p.y)) / (2.0 * M_PI);
+        break;
+    case RT_PLANE: case RT_CUBE:                                                /* :196-205 */
+        u = h->p.x;
+        v = h->p.z;
+        break;
+    case RT_CYLINDER:                                                           /* :339-359 */
+        if (h->face == 0) {
+            u = (go_atan2(h->p.x, h->p.z) + M_PI) / (2.0 * M_PI);
+            v = h->p.y;
+        } else {
+            u = h->p.x;
+            v = h->p.z;
+        }
+        break;
+    }
+    int face = (o->kind == RT_PLANE) ? 0 : h->face;
+    eval_program(-mi - 1, face, u, v, bad, x, cnt);
 }
 
 static int in_shadow(const scene *s, const hit *h, const hitex *x, vec3 ldir, double dist, ray r, counters *cnt) { /* :411-429 */
@@ -339,7 +397,7 @@ static vec3 trace_ray(const scene *s, ray r, int depth, counters *cnt) {        
         return v_lerp(s->bg0, s->bg1, t);
     }
     hitex x;
-    surface_props(s, &h, &x);
+    surface_props(s, &h, &x, cnt);
     cnt->shaded++;
     vec3 lighting = compute_lighting(s, &h, &x, r, cnt);
     const rt_material *mat = x.mat;
@@ -417,7 +475,7 @@ static int convert_scene(const rt_scene *in, scene *s) {
         if (src->kind < 0 || src->kind >= RT_NUM_KINDS) return RT_E_INVALID;
         for (int f = 0; f < RT_MAX_FACES; f++) {
             o->material[f] = src->material[f];
-            if (src->material[f] < 0 || src->material[f] >= in->num_materials) return RT_E_INVALID;
+            if (src->material[f] >= in->num_materials || src->material[f] < -in->num_programs) return RT_E_INVALID;
         }
         if (src->has_transform) {                                               /* :757-762 */
             memcpy(o->o2w.m, src->transform, sizeof(double) * 16);
@@ -501,6 +559,7 @@ static void *worker(void *arg) {
     j->sum.secondary += cnt.secondary;
     j->sum.shadow += cnt.shadow;
     j->sum.shaded += cnt.shaded;
+    j->sum.surface_errors += cnt.surface_errors;
     for (int k = 0; k < 4; k++) { j->sum.tests[k] += cnt.tests[k]; j->sum.shadow_tests[k] += cnt.shadow_tests[k]; }
     pthread_mutex_unlock(&j->lock);
     return NULL;
@@ -538,6 +597,7 @@ int oracle_render_rows(const rt_scene *in, int y0, int y1, int threads, uint8_t 
         st->secondary_rays = j.sum.secondary;
         st->shadow_rays = j.sum.shadow;
         st->shaded_hits = j.sum.shaded;
+        st->surface_errors = j.sum.surface_errors;
         for (int k = 0; k < 4; k++) { st->tests[k] = j.sum.tests[k]; st->shadow_tests[k] = j.sum.shadow_tests[k]; }
     }
     free_scene(&s);
@@ -575,7 +635,9 @@ int oracle_surface_normal(const rt_scene *in, int idx, int face, const double po
     if (s.obj[idx].kind == RT_CUBE && (face < 0 || face >= 6)) { free_scene(&s); return RT_E_INVALID; }    /* :243-245 */
     hit h = {idx, 0, V(point_obj[0], point_obj[1], point_obj[2]), face};
     hitex x;
-    surface_props(&s, &h, &x);
+    counters cnt;
+    memset(&cnt, 0, sizeof cnt);
+    surface_props(&s, &h, &x, &cnt);
     nw[0] = x.nw.x; nw[1] = x.nw.y; nw[2] = x.nw.z;
     pw[0] = x.pw.x; pw[1] = x.pw.y; pw[2] = x.pw.z;
     free_scene(&s);
@@ -584,6 +646,8 @@ int oracle_surface_normal(const rt_scene *in, int idx, int face, const double po
 
 /* Go math restatements exposed for tests. */
 double oracle_go_pow(double x, double y) { return go_pow(x, y); }
+double oracle_go_acos(double x) { return go_acos(x); }
+double oracle_go_atan2(double y, double x) { return go_atan2(y, x); }
 double oracle_go_tan(double x) { return go_tan(x); }
 double oracle_go_sin(double x) { return go_sin(x); }
 double oracle_go_cos(double x) { return go_cos(x); }

@@ -146,3 +146,90 @@ def test_interleaved_tile_rows_equal_full_frame(ctx, world):
     torch.cuda.synchronize()
     frame = rt.dist.deinterleave(slabs, 180).cpu().numpy()
     assert_same(frame, full, "interleaved world %d" % world)
+
+
+# ---- GML programs with closure surfaces (device VM), pinned by the goldens ----
+GML = os.path.join(os.path.dirname(__file__), "golden", "gml")
+CYL = {"cylinder0.ppm": "front", "cylinder1.ppm": "bottom", "cylinder2.ppm": "top", "cylinder3.ppm": "back"}
+
+
+def _gml_args(name):
+    from go_raytracer_amd import gml
+    rendered, _ = gml.run_file(os.path.join(GML, name + ".gml"))
+    return [a for a, _ in rendered]
+
+
+@pytest.mark.parametrize("name", ["sphere", "cube"])
+def test_gml_closure_scene_matches_reference_golden(ctx, name):
+    args = _gml_args(name)[0]
+    packed = rt.scene.convert(args)
+    assert packed.scene.num_programs > 0
+    img, st = render(ctx, packed)
+    gold = np.asarray(Image.open(os.path.join(GOLDEN, "example_%s.png" % name)).convert("RGB"))
+    assert st.surface_errors == 0
+    assert_same(img[..., :3], gold, "%s vs example_%s.png" % (name, name))
+
+
+def test_gml_cylinder_views_match_reference_goldens(ctx):
+    for args in _gml_args("cylinder"):
+        packed = rt.scene.convert(args)
+        img, st = render(ctx, packed)
+        gold = np.asarray(Image.open(os.path.join(GOLDEN, "example_cylinder_%s.png" % CYL[args.file])).convert("RGB"))
+        assert st.surface_errors == 0
+        assert_same(img[..., :3], gold, args.file)
+
+
+@pytest.mark.parametrize("name,w,h", [("sphere", 192, 120), ("cube", 128, 96)])
+def test_gml_closure_scene_matches_oracle_with_counters(ctx, name, w, h):
+    args = _gml_args(name)[0]
+    args.width, args.height = w, h
+    packed = rt.scene.convert(args)
+    img, st = render(ctx, packed)
+    ref, ost = oracle_bind.render_rows(packed)
+    assert_same(img, ref, name)
+    assert st.as_dict() == ost.as_dict()
+
+
+def test_gml_closure_errors_are_counted(ctx):
+    # texture lookup out of range for |u| >= 1.5 (get on a 2-element array)
+    from go_raytracer_amd import gml
+    src = """
+    [ 0.0 1.0 ] /tab
+    { /v /u /face tab u floor get /c c c c point 1.0 0.0 1.0 } plane 0.0 -1.0 0.0 translate /p
+    0.2 0.2 0.2 point [ ] p 1 90.0 64 48 "x.ppm" render
+    """
+    rendered, _ = gml.run_text(src)
+    packed = rt.scene.convert(rendered[0][0])
+    _, st = render(ctx, packed)
+    _, ost = oracle_bind.render_rows(packed)
+    assert st.surface_errors > 0 and st.surface_errors == ost.surface_errors
+
+
+@pytest.mark.parametrize("name", ["sphere", "cube", "cylinder"])
+def test_surface_vm_matches_interpreter(ctx, name):
+    """Every compiled closure, on the device VM, equals the GML interpreter
+    (restatement of EvalSurfaceFn) bit for bit on random (face, u, v)."""
+    import random
+    from go_raytracer_amd import gml
+    rendered, _ = gml.run_file(os.path.join(GML, name + ".gml"))
+    args, e = rendered[0]
+    packed = rt.scene.convert(args)
+    ctx.set_scene(packed)
+    rng = random.Random(7)
+    n = 4000
+    face = [rng.choice([0, 1, 2, 3, 4, 5]) for _ in range(n)]
+    us = [rng.choice([rng.uniform(-3, 3), 0.5, -0.5, 0.0, 1.5, 2.25]) for _ in range(n)]
+    vs = [rng.choice([rng.uniform(-3, 3), 0.5, -0.5, 0.0, 2.5]) for _ in range(n)]
+    sfs = packed.programs[3]
+    for pi, sf in enumerate(sfs):
+        out, err = ctx.debug_run_surface(pi, face, us, vs)
+        for k in range(n):
+            try:
+                m = gml.eval_surface_fn(face[k], us[k], vs[k], args.state.clone(), sf)
+                want = list(m.color) + [m.reflectivity, m.fuzziness, m.transparency, m.refractive_index,
+                                        m.kd, m.ks, m.specular_exponent]
+                assert err[k] == 0, (name, pi, face[k], us[k], vs[k])
+                assert np.array_equal(np.array(want).view(np.uint64), out[k].view(np.uint64)), \
+                    (name, pi, face[k], us[k], vs[k], want, list(out[k]))
+            except gml.GMLError:
+                assert err[k] == 1, (name, pi, face[k], us[k], vs[k])
