@@ -23,9 +23,46 @@ __device__ __forceinline__ d3 mul(d3 a, d3 b) { return mk(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }   // vec.go:48
 __device__ __forceinline__ d3 scale(d3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }    // vec.go:70
 __device__ __forceinline__ double len(d3 v) { return __builtin_sqrt(v.x * v.x + v.y * v.y + v.z * v.z); }  // vec.go:95
+// Shared-denominator division, bit-identical to `/`. hipcc lowers an FP64
+// division on gfx950 to
+//   d' = div_scale(d); y = rcp(d'); 2x { e = fma(-d', y, 1); y = fma(y, e, y) }
+//   n' = div_scale(n); q = n' * y; r = fma(-d', q, n'); div_fmas(r, y, q); div_fixup
+// When 2^-400 <= |n|, |d| < 2^400 both div_scale steps are the identity
+// (VCC = 0, so div_fmas is a plain fma) and div_fixup returns its input, so
+// the reciprocal refinement depends on d alone and can be shared by several
+// numerators: 5 instructions once + 3 per quotient instead of 11 each.
+// Lanes outside that range take the real division in a wave-uniform branch.
+__device__ __forceinline__ bool div_safe(double x) {
+  const uint32_t h = (uint32_t)__double2hiint(x) & 0x7fffffffu;
+  return h - 0x26F00000u < 0x32000000u;  // biased exponent in [623, 1423)
+}
+__device__ __forceinline__ double rcp_refined(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-d, y, 1.0);
+  return __builtin_fma(y, e, y);
+}
+__device__ __forceinline__ double div_rcp(double n, double d, double y) {
+  const double q = n * y;
+  return __builtin_fma(__builtin_fma(-d, q, n), y, q);
+}
+#ifndef RT_SHARED_DIV
+#define RT_SHARED_DIV 0  // measured neutral on C2/C3/C4 (code size vs. saved FP64 ops)
+#endif
 __device__ __forceinline__ d3 norm(d3 v) {                                                        // vec.go:78
   double m = __builtin_sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+#if RT_SHARED_DIV
+  const double y = rcp_refined(m);
+  d3 r = mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
+  const bool ok = div_safe(m) && div_safe(v.x) && div_safe(v.y) && div_safe(v.z);
+  if (__any(!ok)) {
+    if (!ok) r = mk(v.x / m, v.y / m, v.z / m);
+  }
+  return r;
+#else
   return mk(v.x / m, v.y / m, v.z / m);
+#endif
 }
 __device__ __forceinline__ d3 neg(d3 v) { return mk(-v.x, -v.y, -v.z); }                          // vec.go:87
 __device__ __forceinline__ d3 lerp(d3 a, d3 b, double t) {                                        // vec.go:56
@@ -76,7 +113,7 @@ __device__ __forceinline__ bool go_is_odd_int(double x) {
 // reference's specular n and Schlick's 5) are reproduced exactly; the
 // fractional part goes through exp/log, whose Go amd64 assembly is not
 // restated (parity for fractional specular exponents is unpinned).
-__device__ __forceinline__ double go_pow(double x, double y) {
+__device__ __noinline__ double go_pow_general(double x, double y) {
   if (y == 0 || x == 1) return 1;
   if (y == 1) return x;
   if (__builtin_isnan(x) || __builtin_isnan(y)) return __builtin_nan("");
@@ -141,6 +178,41 @@ __device__ __forceinline__ double go_pow(double x, double y) {
     ae = -ae;
   }
   return ldexp(a1, ae);
+}
+
+// math.Pow as computeLighting calls it: Pow(max(0, N.H), n) with a finite
+// positive base and, in practice, an integer exponent. For 0 < x < inf,
+// x != 1 and integer 2 <= y < 2^31 every special case of go_pow_general is
+// false, yf == 0 and y > 0, so it reduces to the Frexp / repeated-squaring /
+// Ldexp loop below (same ops, same order); x == 0 takes its zero case. The
+// general routine (with the exp/log fraction path) stays out of line: inlined
+// it doubled the kernel's register spills.
+__device__ __forceinline__ double go_pow(double x, double y) {
+  if (x > 0 && x < __builtin_inf() && x != 1 && y >= 2 && y < 2147483648.0 && __builtin_floor(y) == y) {
+    int xe;
+    double x1 = frexp(x, &xe);
+    double a1 = 1.0;
+    int ae = 0;
+    for (int i = (int)y; i != 0; i >>= 1) {
+      if (xe < -(1 << 12) || (1 << 12) < xe) {
+        ae += xe;
+        break;
+      }
+      if ((i & 1) == 1) {
+        a1 *= x1;
+        ae += xe;
+      }
+      x1 *= x1;
+      xe <<= 1;
+      if (x1 < .5) {
+        x1 += x1;
+        xe--;
+      }
+    }
+    return ldexp(a1, ae);
+  }
+  if (x == 0 && y > 0) return (signbit64(x) && go_is_odd_int(y)) ? x : 0.0;
+  return go_pow_general(x, y);
 }
 
 // math/rand/v2 PCG (pcg.go): 128-bit LCG, DXSM output; Rand.Float64.

@@ -36,6 +36,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -73,7 +74,9 @@ using namespace rt;
 // geo    [nobj][GEO]  0..11 WorldToObject rows 0-2; planes: 12..14 normal, 15 D;
 //                     bounded kinds: 12..13 = 4 floats (centre xyz, padded
 //                     radius^2) of a world-space bounding sphere (culling only)
-// shade  [nobj][SHD]  0..11 ObjectToWorld rows 0-2, 12..29 NormalWorld per face
+// shade  [nobj][SHD]  0..11 ObjectToWorld rows 0-2, 12..29 NormalWorld per face;
+//                     planes: 16..19 = 8 floats of the world-space plane for
+//                     culling (see may_hit_plane)
 // mats   [nmat][MAT]  0..2 colour, 3 reflectivity, 4..5 baked fuzz offset
 //                     (fuzz*cos^2, fuzz*sin^2; raytracer.go:517-521), 6 fuzz>=0,
 //                     7 transparency, 8 ior, 9 kd, 10 ks, 11 specular exponent
@@ -329,6 +332,34 @@ __device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g)
   return qx * qx + qy * qy + qz * qz <= b[3];
 }
 
+// Conservative FP32 test for a plane: can the segment o + t*d, 0 < t < tmax,
+// cross the plane? c = world-space plane (A^T n, n.b + D for WorldToObject
+// p -> A p + b) followed by its term-magnitude scale (sum_r |n_r||a_rc|,
+// sum_r |n_r||b_r| + |D|). The reference decides a hit from the signs of
+// f(0) = n.o_obj + D and f(tmax) (t = -f(0)/denom compared with tmax), each
+// computed in FP64 with error ~1e-15 of that scale; here both are evaluated
+// in FP32 and `false` needs them to agree in sign with a 1e-4 margin, so the
+// exact test misses (or cannot beat the current best). tmax >= 1e30 means no
+// bound: then f(0) and the slope must agree in sign (the root lies behind).
+__device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, const double* sh) {
+  const float* c = reinterpret_cast<const float*>(sh + 16);
+  const float f0 = c[0] * o.x + c[1] * o.y + c[2] * o.z + c[3];
+  const float sl = c[0] * d.x + c[1] * d.y + c[2] * d.z;
+  const float a0 = c[4] * __builtin_fabsf(o.x) + c[5] * __builtin_fabsf(o.y) + c[6] * __builtin_fabsf(o.z) + c[7];
+  const float a1 = c[4] * __builtin_fabsf(d.x) + c[5] * __builtin_fabsf(d.y) + c[6] * __builtin_fabsf(d.z);
+  float f1, m0, m1;
+  if (tmax >= 1e30f) {
+    f1 = sl;
+    m0 = 1e-4f * a0 + 1e-30f;
+    m1 = 1e-4f * a1 + 1e-30f;
+  } else {
+    f1 = f0 + tmax * sl;
+    m0 = 1e-4f * (a0 + tmax * a1) + 1e-30f;
+    m1 = m0;
+  }
+  return !((f0 > m0 && f1 > m1) || (f0 < -m0 && f1 < -m1));
+}
+
 // Diagnostic build only (-DRT_PHASE_TIMING): wave cycles per phase, stamped
 // with s_memtime into per-wave scalar sums; never enabled in the product.
 #ifdef RT_PHASE_TIMING
@@ -562,7 +593,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   unsigned int pool_next = 0, pool_end = 0;
   bool exhausted = false;
   uint64_t c_shadow = 0, c_traced = 0, c_shaded = 0, c_surferr = 0;
-  uint64_t c_stest[4] = {0, 0, 0, 0};
+  // shadow tests per kind: four scalars (a dynamically indexed array would
+  // live in scratch and put a load/store pair on every object iteration)
+  uint64_t c_st0 = 0, c_st1 = 0, c_st2 = 0, c_st3 = 0;
 #ifdef RT_PHASE_TIMING
   uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -740,10 +773,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         const double* g = S.geo + (size_t)i * GEO;
         bool test = tr;
 #if RT_CULL
-        if (k != RT_PLANE) {
+        {
           // an object entered beyond the lane's current best cannot win (strict <)
           float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
-          test = test && may_hit(of, df, tmax, g);
+          test = test && (k != RT_PLANE ? may_hit(of, df, tmax, g) : may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
           if (!__any(test)) continue;
         }
 #endif
@@ -879,12 +912,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         const int k = S.kind[i];
         const double* g = S.geo + (size_t)i * GEO;
         bool test = open && i != hit_i;
-        c_stest[k] += popc_ballot(test);
-#if RT_CULL
-        if (k != RT_PLANE) {
-          test = test && may_hit(sof, sdf, stmax, g);
-          if (!__any(test)) continue;
+        {
+          const uint64_t n = popc_ballot(test);
+          c_st0 += k == 0 ? n : 0;
+          c_st1 += k == 1 ? n : 0;
+          c_st2 += k == 2 ? n : 0;
+          c_st3 += k == 3 ? n : 0;
         }
+#if RT_CULL
+        test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g) : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+        if (!__any(test)) continue;
 #endif
         if (test) {
           double t;
@@ -1004,7 +1041,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     atomicAdd(P.stats + ST_SHADOW, (unsigned long long)c_shadow);
     atomicAdd(P.stats + ST_SHADED, (unsigned long long)c_shaded);
     atomicAdd(P.stats + ST_SURFERR, (unsigned long long)c_surferr);
-    for (int k = 0; k < 4; k++) atomicAdd(P.stats + ST_STESTS + k, (unsigned long long)c_stest[k]);
+    atomicAdd(P.stats + ST_STESTS + 0, (unsigned long long)c_st0);
+    atomicAdd(P.stats + ST_STESTS + 1, (unsigned long long)c_st1);
+    atomicAdd(P.stats + ST_STESTS + 2, (unsigned long long)c_st2);
+    atomicAdd(P.stats + ST_STESTS + 3, (unsigned long long)c_st3);
   }
 }
 
@@ -1396,6 +1436,27 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       g[14] = o.plane_normal[2];
       g[15] = dv;
       for (int k = 0; k < 3; k++) sh[12 + k] = nw[k];
+      // world-space plane + term scale for may_hit_plane (shade 16..19)
+      const double* n = o.plane_normal;
+      float* c = reinterpret_cast<float*>(&sh[16]);
+      double dabs = std::fabs(dv), dw = dv;
+      for (int k = 0; k < 3; k++) {
+        double wk = 0.0, ak = 0.0;
+        for (int r = 0; r < 3; r++) {
+          wk += n[r] * w2o.m[r][k];
+          ak += std::fabs(n[r]) * std::fabs(w2o.m[r][k]);
+        }
+        c[k] = (float)wk;
+        c[4 + k] = (float)(ak * 1.001);
+      }
+      for (int r = 0; r < 3; r++) {
+        dw += n[r] * w2o.m[r][3];
+        dabs += std::fabs(n[r]) * std::fabs(w2o.m[r][3]);
+      }
+      c[3] = (float)dw;
+      c[7] = (float)(dabs * 1.001);
+      if (!std::isfinite(c[0] + c[1] + c[2] + c[3] + c[4] + c[5] + c[6] + c[7]))
+        for (int k = 0; k < 8; k++) c[k] = std::numeric_limits<float>::quiet_NaN();  // never culls
     } else if (o.kind == RT_CUBE) {
       for (int f = 0; f < 6; f++) {
         double nw[3], dv;

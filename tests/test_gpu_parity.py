@@ -233,3 +233,15 @@ def test_surface_vm_matches_interpreter(ctx, name):
                     (name, pi, face[k], us[k], vs[k], want, list(out[k]))
             except gml.GMLError:
                 assert err[k] == 1, (name, pi, face[k], us[k], vs[k])
+
+
+def test_shared_reciprocal_division_is_bit_exact():
+    """rt_device.h norm(): the shared-reciprocal quotients equal IEEE `/` for
+    ~270M random vectors (safe range, its edges, denormals, specials)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "hip", "div_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(exe)], check=True)
+    r = subprocess.run([exe, "256"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert '"mismatches": 0' in r.stdout
