@@ -114,7 +114,14 @@ struct Params {
   int frames;  // stack frames per lane (depth - 1, >= 1)
   double vw, vh;
   double amb[3], bg0[3], bg1[3];
+  // BVH flavour (scenes with many bounded objects)
+  const float* bvh_nodes;  // [n][BN]: lo xyz, hi xyz, then int first, count, minidx, axis
+  const int* bvh_obj;      // leaf object indices (ascending within a leaf)
+  const int* planes;       // unbounded objects, ascending index
+  const uint32_t* pref;    // [nobj + 1][4]: objects of each kind with index < i
+  int nplanes, bvh_stack_off;
 };
+enum { BN = 12, BVH_STACK = 64 };
 
 struct Ray {
   d3 o, d;
@@ -323,13 +330,35 @@ struct F3 {
   float x, y, z;
 };
 __device__ __forceinline__ F3 f3(d3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
-__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g) {
+// `slack` (ray_slack) widens the radius by the FP32 rounding scale of the
+// ray origin, so origins far from the object stay conservative.
+__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g, float slack) {
   const float* b = reinterpret_cast<const float*>(g + 12);
   float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
   float tc = ox * d.x + oy * d.y + oz * d.z;
   tc = fminf(fmaxf(tc, 0.0f), tmax);
   float qx = ox - tc * d.x, qy = oy - tc * d.y, qz = oz - tc * d.z;
-  return qx * qx + qy * qy + qz * qz <= b[3];
+  const float R = b[3] + slack;
+  return qx * qx + qy * qy + qz * qz <= R * R;
+}
+__device__ __forceinline__ float ray_slack(F3 o) {
+  return 1e-5f * (1.0f + __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z));
+}
+// Conservative FP32 slab test against a BVH node box (built from the padded
+// bounding spheres, rounded outwards), widened by the lane's slack. A
+// component 0 * inf = NaN is ignored by fminf/fmaxf, i.e. a ray parallel to a
+// slab is constrained only by the other axes (it lies on or beyond the
+// widened face otherwise).
+__device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax, const float* nb) {
+  const float x0 = (nb[0] - slack - o.x) * id.x, x1 = (nb[3] + slack - o.x) * id.x;
+  const float y0 = (nb[1] - slack - o.y) * id.y, y1 = (nb[4] + slack - o.y) * id.y;
+  const float z0 = (nb[2] - slack - o.z) * id.z, z1 = (nb[5] + slack - o.z) * id.z;
+  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+  return tn <= tf && tf >= 0.0f && tn <= tmax;
+}
+__device__ __forceinline__ F3 f3_rcp(F3 d) {
+  return F3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
 }
 
 // Conservative FP32 test for a plane: can the segment o + t*d, 0 < t < tmax,
@@ -524,9 +553,9 @@ struct View {
   const int* objmat;
 };
 
-template <bool LDS>
+template <bool LDS, bool BVH>
 #ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 3  // 168 VGPRs -> 3 waves/SIMD (measured best on C3/C4)
+#define RT_MIN_WAVES 4  // 128 VGPRs -> 4 waves/SIMD (C3 on par with 3, C4 +10%)
 #endif
 __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char* __restrict__ blob, Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -596,6 +625,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // shadow tests per kind: four scalars (a dynamically indexed array would
   // live in scratch and put a load/store pair on every object iteration)
   uint64_t c_st0 = 0, c_st1 = 0, c_st2 = 0, c_st3 = 0;
+  // BVH flavour: per-lane shadow-test counts (derived per shadow ray)
+  uint64_t l_st0 = 0, l_st1 = 0, l_st2 = 0, l_st3 = 0;
+  int* bstk = reinterpret_cast<int*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
 #ifdef RT_PHASE_TIMING
   uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -765,31 +797,66 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       bool found = false;
       double best_t = 0.0;
       int best_i = 0, best_f = 0;
-#if RT_CULL
       const F3 of = f3(ray.o), df = f3(ray.d);
-#endif
-      for (int i = 0; i < P.nobj; i++) {
+      const float slack = ray_slack(of);
+      // One closestHit candidate (object i, wave-uniform) for the lanes in `act`.
+      // The linear loop visits objects in index order (strict <, the first
+      // index wins ties); the BVH visits them in any order and breaks ties on
+      // the index explicitly, which selects the same object.
+      auto trace_obj = [&](int i, bool act) {
         const int k = S.kind[i];
         const double* g = S.geo + (size_t)i * GEO;
-        bool test = tr;
+        bool test = act;
 #if RT_CULL
-        {
-          // an object entered beyond the lane's current best cannot win (strict <)
-          float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
-          test = test && (k != RT_PLANE ? may_hit(of, df, tmax, g) : may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
-          if (!__any(test)) continue;
-        }
+        // an object entered beyond the lane's current best cannot win (strict <)
+        const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+        test = test && (k != RT_PLANE ? may_hit(of, df, tmax, g, slack)
+                                      : may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
+        if (!__any(test)) return;
 #endif
         if (test) {
           double t;
           int f;
           if (object_hit(k, g, ray, t, f)) {
-            if (!found || t < best_t) {
+            if (!found || t < best_t || (BVH && t == best_t && i < best_i)) {
               found = true;
               best_t = t;
               best_i = i;
               best_f = f;
             }
+          }
+        }
+      };
+      if constexpr (!BVH) {
+        for (int i = 0; i < P.nobj; i++) trace_obj(i, tr);
+      } else {
+        for (int p = 0; p < P.nplanes; p++) trace_obj(P.planes[p], tr);
+        const F3 idf = f3_rcp(df);
+        int ssp = 1;
+        if (lane == 0) bstk[0] = 0;
+        while (ssp > 0) {
+          ssp--;
+          const int node = __builtin_amdgcn_readfirstlane(bstk[ssp]);
+          const float* nb = P.bvh_nodes + (size_t)node * BN;
+          const int* ni = reinterpret_cast<const int*>(nb + 6);
+          const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+          const bool act = tr && may_hit_box(of, idf, slack, tmax, nb);
+          const uint64_t am = __ballot(act);
+          if (am == 0) continue;
+          const int first = ni[0], count = ni[1];
+          if (count > 0) {
+            for (int j = first; j < first + count; j++) trace_obj(P.bvh_obj[j], act);
+          } else {
+            // near child first: the side most active lanes travel from
+            const int axis = ni[3];
+            const float da = axis == 0 ? df.x : (axis == 1 ? df.y : df.z);
+            const uint64_t neg = __ballot(act && da < 0.0f);
+            const bool hi_first = 2 * __popcll(neg) > __popcll(am);
+            if (lane == 0) {
+              bstk[ssp] = hi_first ? first : first + 1;
+              bstk[ssp + 1] = hi_first ? first + 1 : first;
+            }
+            ssp += 2;
           }
         }
       }
@@ -902,33 +969,93 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       Ray sr;
       sr.o = sorig;
       sr.d = ldir;
-#if RT_CULL
       const F3 sof = f3(sorig), sdf = f3(ldir);
+      const float sslack = ray_slack(sof);
       // occluders must lie within t < dist / |ray.d| (raytracer.go:424)
       const float stmax = (float)(dist / rlen) * 1.0001f + 1e-4f;
-#endif
-      for (int i = 0; i < P.nobj; i++) {
-        if (!__any(open)) break;
-        const int k = S.kind[i];
-        const double* g = S.geo + (size_t)i * GEO;
-        bool test = open && i != hit_i;
-        {
-          const uint64_t n = popc_ballot(test);
-          c_st0 += k == 0 ? n : 0;
-          c_st1 += k == 1 ? n : 0;
-          c_st2 += k == 2 ? n : 0;
-          c_st3 += k == 3 ? n : 0;
-        }
-#if RT_CULL
-        test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g) : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
-        if (!__any(test)) continue;
-#endif
-        if (test) {
-          double t;
-          int f;
-          if (object_hit(k, g, sr, t, f)) {
-            if (t * rlen < dist) open = false;
+      if constexpr (!BVH) {
+        for (int i = 0; i < P.nobj; i++) {
+          if (!__any(open)) break;
+          const int k = S.kind[i];
+          const double* g = S.geo + (size_t)i * GEO;
+          bool test = open && i != hit_i;
+          {
+            const uint64_t n = popc_ballot(test);
+            c_st0 += k == 0 ? n : 0;
+            c_st1 += k == 1 ? n : 0;
+            c_st2 += k == 2 ? n : 0;
+            c_st3 += k == 3 ? n : 0;
           }
+#if RT_CULL
+          test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
+                                        : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!__any(test)) continue;
+#endif
+          if (test) {
+            double t;
+            int f;
+            if (object_hit(k, g, sr, t, f)) {
+              if (t * rlen < dist) open = false;
+            }
+          }
+        }
+      } else {
+        // The reference stops at the first occluder in index order and its
+        // test count is #{i <= that index, i != hit}; the BVH finds the
+        // lowest-index occluder (pruning subtrees whose smallest index is not
+        // lower than the best so far) and derives the count from prefix
+        // counts per kind. The shadow verdict is the same either way.
+        int occ = 0x7fffffff;
+        auto shadow_obj = [&](int i, bool act) {
+          const int k = S.kind[i];
+          const double* g = S.geo + (size_t)i * GEO;
+          bool test = act && i != hit_i && i < occ;
+          test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
+                                        : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!__any(test)) return;
+          if (test) {
+            double t;
+            int f;
+            if (object_hit(k, g, sr, t, f)) {
+              if (t * rlen < dist) occ = i;
+            }
+          }
+        };
+        for (int p = 0; p < P.nplanes; p++) shadow_obj(P.planes[p], hit);
+        const F3 sidf = f3_rcp(sdf);
+        int ssp = 1;
+        if (lane == 0) bstk[0] = 0;
+        while (ssp > 0) {
+          ssp--;
+          const int node = __builtin_amdgcn_readfirstlane(bstk[ssp]);
+          const float* nb = P.bvh_nodes + (size_t)node * BN;
+          const int* ni = reinterpret_cast<const int*>(nb + 6);
+          const bool act = hit && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb);
+          if (!__any(act)) continue;
+          const int first = ni[0], count = ni[1];
+          if (count > 0) {
+            for (int j = first; j < first + count; j++) shadow_obj(P.bvh_obj[j], act);
+          } else {
+            // lower-index subtree first: it can prune the other
+            const int* li = reinterpret_cast<const int*>(P.bvh_nodes + (size_t)first * BN + 6);
+            const int* ri = reinterpret_cast<const int*>(P.bvh_nodes + (size_t)(first + 1) * BN + 6);
+            const bool right_first = ri[2] < li[2];
+            if (lane == 0) {
+              bstk[ssp] = right_first ? first : first + 1;
+              bstk[ssp + 1] = right_first ? first + 1 : first;
+            }
+            ssp += 2;
+          }
+        }
+        open = hit && occ == 0x7fffffff;
+        if (hit) {
+          const int end = occ == 0x7fffffff ? P.nobj : occ + 1;
+          const uint4 pe = *reinterpret_cast<const uint4*>(P.pref + (size_t)end * 4);
+          const int hk = hit_i < end ? S.kind[hit_i] : -1;
+          l_st0 += pe.x - (hk == 0 ? 1u : 0u);
+          l_st1 += pe.y - (hk == 1 ? 1u : 0u);
+          l_st2 += pe.z - (hk == 2 ? 1u : 0u);
+          l_st3 += pe.w - (hk == 3 ? 1u : 0u);
         }
       }
       PH_MARK(4);
@@ -1046,6 +1173,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     atomicAdd(P.stats + ST_STESTS + 2, (unsigned long long)c_st2);
     atomicAdd(P.stats + ST_STESTS + 3, (unsigned long long)c_st3);
   }
+  if constexpr (BVH) {
+    atomicAdd(P.stats + ST_STESTS + 0, (unsigned long long)l_st0);
+    atomicAdd(P.stats + ST_STESTS + 1, (unsigned long long)l_st1);
+    atomicAdd(P.stats + ST_STESTS + 2, (unsigned long long)l_st2);
+    atomicAdd(P.stats + ST_STESTS + 3, (unsigned long long)l_st3);
+  }
 }
 
 // Diagnostic: run surface program `prog` of the current scene on n inputs.
@@ -1060,8 +1193,10 @@ __global__ void rt_debug_vm_kernel(const char* __restrict__ blob, int off_code, 
   err[i] = run_vm(code, consts, entry[prog], face[i], u[i], v[i], out + (size_t)i * 10) ? 1 : 0;
 }
 
-template __global__ void rt_render_kernel<true>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<false>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<true, false>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<false, false>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<true, true>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<false, true>(const char* __restrict__, Params);
 // ===========================================================================
 // Host side: scene conversion (raytracer.go:724-830) and the C ABI
 // ===========================================================================
@@ -1220,6 +1355,90 @@ struct DevScene {
   int off_geo = 0, off_shade = 0, off_mats = 0, off_lights = 0, off_kind = 0, off_objmat = 0;
   std::vector<int> kinds;  // host copy for the per-kind test counts
   int off_code = 0, off_consts = 0, off_entry = 0, num_programs = 0;
+  // BVH flavour: one device buffer nodes | leaf objects | planes | prefix counts
+  char* accel = nullptr;
+  bool use_bvh = false;
+  int nplanes = 0, nnodes = 0;
+  size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_pref = 0;
+};
+
+// Scenes with at least this many bounded objects use the BVH flavour.
+#ifndef RT_BVH_MIN
+#define RT_BVH_MIN 12
+#endif
+
+float f_down(double x) {
+  float f = (float)x;
+  return (double)f > x ? std::nextafter(f, -std::numeric_limits<float>::infinity()) : f;
+}
+float f_up(double x) {
+  float f = (float)x;
+  return (double)f < x ? std::nextafter(f, std::numeric_limits<float>::infinity()) : f;
+}
+
+// Median-split BVH over the bounded objects' padded bounding spheres (boxes
+// rounded outwards to FP32). Median splits keep the depth at ~log2(n / 4), far
+// below the device stack (BVH_STACK entries); leaves hold <= 4 objects in
+// ascending index order.
+struct BvhBuild {
+  const std::vector<double>* c;  // [n][3] centres
+  const std::vector<double>* r;  // [n] radii
+  std::vector<int> ord;          // object indices
+  std::vector<float> nodes;      // [m][BN]
+  int max_depth = 0;
+
+  int alloc() {
+    nodes.resize(nodes.size() + BN, 0.0f);
+    return (int)(nodes.size() / BN) - 1;
+  }
+  void build(int node, int lo, int hi, int depth) {
+    max_depth = std::max(max_depth, depth);
+    double bl[3] = {1e300, 1e300, 1e300}, bh[3] = {-1e300, -1e300, -1e300};
+    double cl[3] = {1e300, 1e300, 1e300}, ch[3] = {-1e300, -1e300, -1e300};
+    int minidx = 0x7fffffff;
+    for (int j = lo; j < hi; j++) {
+      const int i = ord[j];
+      minidx = std::min(minidx, i);
+      for (int k = 0; k < 3; k++) {
+        const double cc = (*c)[(size_t)i * 3 + k], rr = (*r)[i];
+        bl[k] = std::min(bl[k], cc - rr);
+        bh[k] = std::max(bh[k], cc + rr);
+        cl[k] = std::min(cl[k], cc);
+        ch[k] = std::max(ch[k], cc);
+      }
+    }
+    float* nb = &nodes[(size_t)node * BN];
+    for (int k = 0; k < 3; k++) {
+      nb[k] = f_down(bl[k]);
+      nb[3 + k] = f_up(bh[k]);
+    }
+    int* ni = reinterpret_cast<int*>(nb + 6);
+    ni[2] = minidx;
+    if (hi - lo <= 4) {
+      std::sort(ord.begin() + lo, ord.begin() + hi);
+      ni[0] = lo;
+      ni[1] = hi - lo;
+      ni[3] = 0;
+      return;
+    }
+    int axis = 0;
+    for (int k = 1; k < 3; k++)
+      if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
+    const int mid = (lo + hi) / 2;
+    std::nth_element(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, [&](int a, int b) {
+      const double ca = (*c)[(size_t)a * 3 + axis], cb = (*c)[(size_t)b * 3 + axis];
+      return ca < cb || (ca == cb && a < b);
+    });
+    const int left = alloc();
+    alloc();
+    nb = &nodes[(size_t)node * BN];  // alloc may have moved the storage
+    ni = reinterpret_cast<int*>(nb + 6);
+    ni[0] = left;
+    ni[1] = 0;
+    ni[3] = axis;
+    build(left, lo, mid, depth + 1);
+    build(left + 1, mid, hi, depth + 1);
+  }
 };
 
 int align16(int v) { return (v + 15) & ~15; }
@@ -1260,6 +1479,7 @@ struct DeviceGuard {
 
 void free_scene(DevScene& s) {
   (void)hipFree(s.blob);
+  (void)hipFree(s.accel);
   s = DevScene();
 }
 
@@ -1298,12 +1518,12 @@ int rt_create(int device, rt_context** out) {
   // Persistent grids: as many workgroups as are resident (any extra block just
   // finds the queue drained). The LDS flavour is sized for the LDS budget.
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, WG, LDS_MAX_BYTES) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true, false>, WG, LDS_MAX_BYTES) !=
           hipSuccess || per_cu <= 0)
     per_cu = 2;
   c->grid_lds = c->cus * std::min(per_cu, 8);
   per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false>, WG, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false, false>, WG, 0) != hipSuccess ||
       per_cu <= 0)
     per_cu = 2;
   c->grid_glb = c->cus * std::min(per_cu, 8);
@@ -1385,6 +1605,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
 
   std::vector<double> geo((size_t)s.nobj * GEO, 0.0), shade((size_t)s.nobj * SHD, 0.0);
   std::vector<int> kind(s.nobj), objmat((size_t)s.nobj * OMAT, 0);
+  std::vector<double> bcen((size_t)s.nobj * 3, 0.0), brad((size_t)s.nobj, 0.0);  // padded bounding spheres
   for (int i = 0; i < s.nobj; i++) {
     const rt_object& o = in->objects[i];
     if (o.kind < 0 || o.kind >= RT_NUM_KINDS) return fail(RT_E_INVALID, "unknown scene object type");
@@ -1426,7 +1647,9 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       b[0] = (float)cc[0];
       b[1] = (float)cc[1];
       b[2] = (float)cc[2];
-      b[3] = (float)(rad * rad);
+      b[3] = f_up(rad);
+      for (int k = 0; k < 3; k++) bcen[(size_t)i * 3 + k] = cc[k];
+      brad[i] = rad;
     }
     if (o.kind == RT_PLANE) {
       double nw[3], dv;
@@ -1557,6 +1780,43 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     }
   }
   s.kinds = kind;
+  {
+    // Acceleration structure for scenes with many bounded objects.
+    std::vector<int> bounded, planes;
+    for (int i = 0; i < s.nobj; i++) (kind[i] == RT_PLANE ? planes : bounded).push_back(i);
+    if ((int)bounded.size() >= RT_BVH_MIN) {
+      BvhBuild b;
+      b.c = &bcen;
+      b.r = &brad;
+      b.ord = bounded;
+      b.alloc();
+      b.build(0, 0, (int)bounded.size(), 0);
+      if (b.max_depth + 2 < BVH_STACK) {
+        std::vector<uint32_t> pref((size_t)(s.nobj + 1) * 4, 0u);
+        for (int i = 0; i < s.nobj; i++) {
+          for (int k = 0; k < 4; k++) pref[(size_t)(i + 1) * 4 + k] = pref[(size_t)i * 4 + k];
+          pref[(size_t)(i + 1) * 4 + kind[i]]++;
+        }
+        s.off_nodes = 0;
+        s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
+        s.off_planes = s.off_bobj + ((b.ord.size() * sizeof(int) + 15) & ~(size_t)15);
+        s.off_pref = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
+        std::vector<char> acc(s.off_pref + pref.size() * sizeof(uint32_t), 0);
+        std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
+        std::memcpy(acc.data() + s.off_bobj, b.ord.data(), b.ord.size() * sizeof(int));
+        if (!planes.empty()) std::memcpy(acc.data() + s.off_planes, planes.data(), planes.size() * sizeof(int));
+        std::memcpy(acc.data() + s.off_pref, pref.data(), pref.size() * sizeof(uint32_t));
+        int rc = upload(&s.accel, acc);
+        if (rc != RT_OK) {
+          free_scene(s);
+          return rc;
+        }
+        s.use_bvh = true;
+        s.nplanes = (int)planes.size();
+        s.nnodes = (int)(b.nodes.size() / BN);
+      }
+    }
+  }
   // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
   int frames = std::max(1, s.depth - 1);
   const int waves = c->cus * 8 * WAVES_PER_WG;  // upper bound of any persistent grid
@@ -1600,15 +1860,12 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const bool lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
   const int frames_off = lds ? s.blob_bytes : 0;
   const int vm_off = frames_off + WAVES_PER_WG * RT_LDS_FRAMES * CORE * 64 * (int)sizeof(double);
-  const int shmem = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
+  const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
+  const int shmem = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * (int)sizeof(int) : 0);
+  const void* kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true> : (const void*)rt_render_kernel<true, false>)
+                        : (s.use_bvh ? (const void*)rt_render_kernel<false, true> : (const void*)rt_render_kernel<false, false>);
   int per_cu = 0;
-  if (lds) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, WG, shmem) != hipSuccess)
-      per_cu = 0;
-  } else {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false>, WG, shmem) != hipSuccess)
-      per_cu = 0;
-  }
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, WG, shmem) != hipSuccess) per_cu = 0;
   if (per_cu <= 0) per_cu = 1;
   const int grid = c->cus * std::min(per_cu, 8);
   if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
@@ -1648,6 +1905,14 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     return fail(RT_E_INVALID, "image too large for one launch");
   P.total_slots = (unsigned int)slots;
   P.frames = std::max(1, s.depth - 1);
+  if (s.use_bvh) {
+    P.bvh_nodes = reinterpret_cast<const float*>(s.accel + s.off_nodes);
+    P.bvh_obj = reinterpret_cast<const int*>(s.accel + s.off_bobj);
+    P.planes = reinterpret_cast<const int*>(s.accel + s.off_planes);
+    P.pref = reinterpret_cast<const uint32_t*>(s.accel + s.off_pref);
+    P.nplanes = s.nplanes;
+    P.bvh_stack_off = stack_off;
+  }
   P.vw = s.vw;
   P.vh = s.vh;
   for (int k = 0; k < 3; k++) {
@@ -1657,10 +1922,15 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   }
   HIP_TRY(hipMemsetAsync(c->queue, 0, 256, st));
   HIP_TRY(hipEventRecord(c->ev0, st));
-  if (lds)
-    hipLaunchKernelGGL(rt_render_kernel<true>, dim3(grid), dim3(WG), shmem, st, (const char*)s.blob, P);
+  const char* blob = s.blob;
+  if (lds && s.use_bvh)
+    hipLaunchKernelGGL((rt_render_kernel<true, true>), dim3(grid), dim3(WG), shmem, st, blob, P);
+  else if (lds)
+    hipLaunchKernelGGL((rt_render_kernel<true, false>), dim3(grid), dim3(WG), shmem, st, blob, P);
+  else if (s.use_bvh)
+    hipLaunchKernelGGL((rt_render_kernel<false, true>), dim3(grid), dim3(WG), shmem, st, blob, P);
   else
-    hipLaunchKernelGGL(rt_render_kernel<false>, dim3(grid), dim3(WG), shmem, st, (const char*)s.blob, P);
+    hipLaunchKernelGGL((rt_render_kernel<false, false>), dim3(grid), dim3(WG), shmem, st, blob, P);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   c->timed = true;
