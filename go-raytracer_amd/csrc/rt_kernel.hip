@@ -91,7 +91,7 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8 };
 // material is both reflective and transparent) always live in HBM.
 enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
-enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_SURFERR = 7, ST_COUNT = 8, ST_PHASE = 16, N_PHASE = 8 };
+enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_SURFERR = 7, ST_COUNT = 8, ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24 };
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
 #ifndef RT_LDS_MAX
 #define RT_LDS_MAX (40 * 1024)
@@ -630,6 +630,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   int* bstk = reinterpret_cast<int*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
 #ifdef RT_PHASE_TIMING
   uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t bd_tnodes = 0, bd_snodes = 0, bd_tleaf = 0, bd_sleaf = 0, bd_trays = 0, bd_srays = 0;
+#ifdef RT_COST_MAP
+  uint32_t lane_cost = 0;  // node visits charged to this lane's pixel (diagnostic)
+#endif
 #endif
 
   const double W1 = (double)(P.width - 1), H1 = (double)(P.height - 1);
@@ -658,8 +662,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
             uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
             uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
+#ifdef RT_COST_MAP
+            P.out[pout] = lane_cost;
+            lane_cost = 0;
+#else
             P.out[pout] =
                 (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+#endif
             state = S_IDLE;
           } else {
             need_gen = true;  // next sample ray, generated in one uniform block
@@ -832,6 +841,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       } else {
         for (int p = 0; p < P.nplanes; p++) trace_obj(P.planes[p], tr);
         const F3 idf = f3_rcp(df);
+#ifdef RT_PHASE_TIMING
+        bd_trays++;
+#endif
         int ssp = 1;
         if (lane == 0) bstk[0] = 0;
         while (ssp > 0) {
@@ -842,9 +854,18 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
           const bool act = tr && may_hit_box(of, idf, slack, tmax, nb);
           const uint64_t am = __ballot(act);
+#ifdef RT_PHASE_TIMING
+          bd_tnodes++;
+#ifdef RT_COST_MAP
+          if (tr) lane_cost++;
+#endif
+#endif
           if (am == 0) continue;
           const int first = ni[0], count = ni[1];
           if (count > 0) {
+#ifdef RT_PHASE_TIMING
+            bd_tleaf++;
+#endif
             for (int j = first; j < first + count; j++) trace_obj(P.bvh_obj[j], act);
           } else {
             // near child first: the side most active lanes travel from
@@ -1023,6 +1044,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         };
         for (int p = 0; p < P.nplanes; p++) shadow_obj(P.planes[p], hit);
         const F3 sidf = f3_rcp(sdf);
+#ifdef RT_PHASE_TIMING
+        bd_srays++;
+#endif
         int ssp = 1;
         if (lane == 0) bstk[0] = 0;
         while (ssp > 0) {
@@ -1031,9 +1055,18 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const float* nb = P.bvh_nodes + (size_t)node * BN;
           const int* ni = reinterpret_cast<const int*>(nb + 6);
           const bool act = hit && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb);
+#ifdef RT_PHASE_TIMING
+          bd_snodes++;
+#ifdef RT_COST_MAP
+          if (hit) lane_cost++;
+#endif
+#endif
           if (!__any(act)) continue;
           const int first = ni[0], count = ni[1];
           if (count > 0) {
+#ifdef RT_PHASE_TIMING
+            bd_sleaf++;
+#endif
             for (int j = first; j < first + count; j++) shadow_obj(P.bvh_obj[j], act);
           } else {
             // lower-index subtree first: it can prune the other
@@ -1163,6 +1196,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   if (lane == 0) {
 #ifdef RT_PHASE_TIMING
     for (int k = 0; k < N_PHASE; k++) atomicAdd(P.stats + ST_PHASE + k, (unsigned long long)ph_acc[k]);
+    atomicAdd(P.stats + ST_BVHDIAG + 0, (unsigned long long)bd_tnodes);
+    atomicAdd(P.stats + ST_BVHDIAG + 1, (unsigned long long)bd_snodes);
+    atomicAdd(P.stats + ST_BVHDIAG + 2, (unsigned long long)bd_tleaf);
+    atomicAdd(P.stats + ST_BVHDIAG + 3, (unsigned long long)bd_sleaf);
+    atomicAdd(P.stats + ST_BVHDIAG + 4, (unsigned long long)bd_trays);
+    atomicAdd(P.stats + ST_BVHDIAG + 5, (unsigned long long)bd_srays);
 #endif
     atomicAdd(P.stats + ST_TRACED, (unsigned long long)c_traced);
     atomicAdd(P.stats + ST_SHADOW, (unsigned long long)c_shadow);
@@ -1995,6 +2034,13 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
       fprintf(stderr, "[phase]");
       for (int k = 0; k < N_PHASE; k++) fprintf(stderr, " %s=%.3f", nm[k], (double)ph[k] / (double)tot);
       fprintf(stderr, " total_wave_cycles=%.4g\n", (double)tot);
+      unsigned long long bd[6];
+      HIP_TRY(hipMemcpy(bd, c->stats + ST_BVHDIAG, sizeof bd, hipMemcpyDeviceToHost));
+      if (bd[4] + bd[5])
+        fprintf(stderr, "[bvh] wave traversals trace=%llu shadow=%llu; nodes/traversal trace=%.1f shadow=%.1f; "
+                        "leaves/traversal trace=%.1f shadow=%.1f\n", bd[4], bd[5], (double)bd[0] / (double)std::max(1ull, bd[4]),
+                (double)bd[1] / (double)std::max(1ull, bd[5]), (double)bd[2] / (double)std::max(1ull, bd[4]),
+                (double)bd[3] / (double)std::max(1ull, bd[5]));
     }
   }
 #endif

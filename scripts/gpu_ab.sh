@@ -1,10 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
-grep -q "pytest rc=0" gpurun_out/pytest_gpu.log || exit 1
-B=build_variants
-for c in c3 c4; do
-timeout -k 10 300 python scripts/ab.py --config $c --rounds 7 $B/librtamd_cp.so go-raytracer_amd/csrc/librtamd.so > gpurun_out/ab_$c.log 2>&1 || exit 1
-done
-timeout -k 10 300 python scripts/ab.py --config c5 --width 480 --height 270 --rounds 3 $B/librtamd_cp.so go-raytracer_amd/csrc/librtamd.so > gpurun_out/ab_c5.log 2>&1 || exit 1
+RT_AMD_LIB=build_variants/librtamd_cost.so timeout -k 10 300 python scripts/cost_map.py c5 480 270 gpurun_out/cost_c5.npy > gpurun_out/cost_c5.log 2>&1
