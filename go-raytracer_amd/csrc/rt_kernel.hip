@@ -1500,6 +1500,8 @@ struct rt_context {
   int stack_waves = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  char* ssim_buf = nullptr;  // SSIM kernel weights + per-block partial sums
+  size_t ssim_bytes = 0;
   uint64_t primary_pending = 0;  // host-side count of launched primary rays
 };
 
@@ -1605,6 +1607,7 @@ void rt_destroy(rt_context* c) {
   if (!c) return;
   DeviceGuard guard(c->device);
   free_scene(c->sc);
+  (void)hipFree(c->ssim_buf);
   (void)hipFree(c->jump);
   (void)hipFree(c->queue);
   (void)hipFree(c->stats);
@@ -2130,3 +2133,5 @@ int rt_render(const rt_scene* scene, uint8_t* rgba_out, rt_stats* stats) {
 }
 
 }  // extern "C"
+
+#include "rt_ssim.hip"

@@ -53,6 +53,8 @@ def load_library(path=None):
     l.rt_last_kernel_ms.restype = i
     l.rt_debug_run_surface.argtypes = [vp, i, i, vp, vp, vp, vp, vp]
     l.rt_debug_run_surface.restype = i
+    l.rt_ssim_rgba8.argtypes = [vp, vp, vp, i, i, C.POINTER(C.c_double), vp]
+    l.rt_ssim_rgba8.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
     l.rt_render.restype = i
     if l.rt_abi_version() != 1:
@@ -150,6 +152,32 @@ class RenderContext:
         _check(self.lib.rt_debug_run_surface(self.handle, int(program), n, face.ctypes.data, u.ctypes.data,
                                              v.ctypes.data, out.ctypes.data, err.ctypes.data), "rt_debug_run_surface")
         return out, err
+
+    def ssim(self, a, b):
+        """prim.SSIM (internal/prim/ssim.go:27-182) of two RGBA8 frames on the
+        device. a, b: uint8 [H, W, 4] (or [H, W, 3]) torch tensors or numpy
+        arrays; host arrays are uploaded."""
+        torch = self.torch
+        dev = "cuda:%d" % self.device
+
+        def prep(x):
+            t = x if isinstance(x, torch.Tensor) else torch.from_numpy(np.array(x, dtype=np.uint8, copy=True))
+            if t.dtype != torch.uint8 or t.dim() != 3 or t.shape[2] not in (3, 4):
+                raise ValueError("ssim: expected uint8 [H, W, 3|4] images")
+            t = t.to(dev)
+            if t.shape[2] == 3:
+                t = torch.cat([t, torch.full_like(t[..., :1], 255)], dim=2)
+            return t.contiguous()
+
+        ta, tb = prep(a), prep(b)
+        if ta.shape != tb.shape:
+            raise ValueError("images are not the same size")  # ssim.go:29-31
+        out = C.c_double()
+        stream = torch.cuda.current_stream(self.device)
+        _check(self.lib.rt_ssim_rgba8(self.handle, C.c_void_p(ta.data_ptr()), C.c_void_p(tb.data_ptr()),
+                                      int(ta.shape[1]), int(ta.shape[0]), C.byref(out),
+                                      C.c_void_p(stream.cuda_stream)), "rt_ssim_rgba8")
+        return out.value
 
     def render(self, y0=0, y1=None):
         """Synchronous render of rows [y0, y1) -> numpy uint8 [rows, W, 4]."""

@@ -202,6 +202,14 @@ int rt_last_kernel_ms(rt_context *ctx, double *ms_out);
 int rt_debug_run_surface(rt_context *ctx, int program, int n, const long long *face,
                          const double *u, const double *v, double *out10, int *err);
 
+/* SSIM of two RGBA8 frames in device memory (width x height, stride 4W), the
+ * reference's parity metric prim.SSIM (internal/prim/ssim.go:27-182; used by
+ * raytracer_test.go:42 with threshold 0.99). Synchronous on `stream`.
+ * RT_E_INVALID "images are too small" below 11x11; NaN at exactly 11 wide or
+ * high (no window visited, as in the reference). */
+int rt_ssim_rgba8(rt_context *ctx, const uint8_t *d_a, const uint8_t *d_b, int width, int height,
+                  double *out_ssim, void *stream);
+
 /* Convenience, synchronous whole-frame Render() into host memory
  * (width*height*4 bytes, caller-owned). Uses a cached context on the
  * current device. stats may be NULL. Includes PCIe transfers. */

@@ -1,4 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-RT_AMD_LIB=build_variants/librtamd_cost.so timeout -k 10 300 python scripts/cost_map.py c5 480 270 gpurun_out/cost_c5.npy > gpurun_out/cost_c5.log 2>&1
+timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log

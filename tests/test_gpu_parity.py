@@ -287,3 +287,34 @@ def test_mixed_scenes_match_oracle(ctx, seed, n):
     ref, ost = oracle_bind.render_rows(packed)
     assert_same(img, ref, "mixed seed %d n %d" % (seed, n))
     assert st.as_dict() == ost.as_dict()
+
+
+@pytest.mark.parametrize("h,w,seed", [(100, 100, 1), (37, 23, 2), (192, 256, 3), (12, 12, 4)])
+def test_device_ssim_matches_restatement(ctx, h, w, seed):
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "oracle"))
+    import ssim_ref
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 256, size=(h, w, 4), dtype=np.uint8)
+    b = np.clip(a.astype(np.int32) + rng.integers(-40, 41, size=a.shape), 0, 255).astype(np.uint8)
+    a[..., 3] = b[..., 3] = 255
+    for x, y in ((a, b), (a, a), (b, a)):
+        want = ssim_ref.ssim(x, y)
+        got = ctx.ssim(x, y)
+        assert abs(got - want) <= 1e-12 * abs(want), (got, want)
+
+
+def test_device_ssim_golden_harness(ctx):
+    """The reference's golden check (raytracer_test.go:42: SSIM >= 0.99) on the
+    HIP render of canned.gml; exact bytes give SSIM of an image with itself."""
+    packed = rt.scene.convert(rt.configs.canned())
+    img, _ = render(ctx, packed)
+    gold = np.asarray(Image.open(os.path.join(GOLDEN, "example_canned.png")).convert("RGB"))
+    s = ctx.ssim(img, gold)
+    assert s >= 0.99
+    assert s == ctx.ssim(gold, gold)
+    with pytest.raises(ValueError):
+        ctx.ssim(img[:10], gold)
+    with pytest.raises(rt.render.RenderError):
+        ctx.ssim(img[:10, :10], gold[:10, :10])
+    assert np.isnan(ctx.ssim(img[:11, :40], gold[:11, :40]))
