@@ -555,7 +555,7 @@ struct View {
 
 template <bool LDS, bool BVH>
 #ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 4  // 128 VGPRs -> 4 waves/SIMD (C3 on par with 3, C4 +10%)
+#define RT_MIN_WAVES 3  // 168 VGPRs -> 3 waves/SIMD (C3 on par with 4; C2 -10%, C4 (BVH) -4%)
 #endif
 __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char* __restrict__ blob, Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
