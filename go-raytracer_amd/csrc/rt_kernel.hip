@@ -120,7 +120,13 @@ struct Params {
   const int* planes;       // unbounded objects, ascending index
   const uint32_t* pref;    // [nobj + 1][4]: objects of each kind with index < i
   int nplanes, bvh_stack_off;
+  int cnt_off;    // LDS byte offset of the per-lane event counters [NCNT][WG]
+  int kind_mask;  // bit k: the scene has objects of kind k
 };
+// Per-lane event counters (u64, LDS, fire-and-forget ds_add), reduced once per
+// workgroup at exit: per-wave 64-bit SGPR counters pushed the kernel into
+// SGPR spilling (C2 +33% time, C3 +7%).
+enum { CNT_TRACED = 0, CNT_SHADED = 1, CNT_SURFERR = 2, CNT_ST0 = 3, NCNT = 7 };
 enum { BN = 12, BVH_STACK = 64 };
 
 struct Ray {
@@ -621,12 +627,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // wave-uniform pool and counters
   unsigned int pool_next = 0, pool_end = 0;
   bool exhausted = false;
-  uint64_t c_shadow = 0, c_traced = 0, c_shaded = 0, c_surferr = 0;
-  // shadow tests per kind: four scalars (a dynamically indexed array would
-  // live in scratch and put a load/store pair on every object iteration)
-  uint64_t c_st0 = 0, c_st1 = 0, c_st2 = 0, c_st3 = 0;
-  // BVH flavour: per-lane shadow-test counts (derived per shadow ray)
-  uint64_t l_st0 = 0, l_st1 = 0, l_st2 = 0, l_st3 = 0;
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off);
+  for (int k = 0; k < NCNT; k++) cnt[k * WG + threadIdx.x] = 0;
+  auto cnt_add = [&](int k, uint64_t v) { atomicAdd(&cnt[k * WG + threadIdx.x], (unsigned long long)v); };
   int* bstk = reinterpret_cast<int*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
 #ifdef RT_PHASE_TIMING
   uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -881,7 +884,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           }
         }
       }
-      c_traced += popc_ballot(tr);
+      if (tr) cnt_add(CNT_TRACED, 1);
       PH_MARK(1);
       d3 res = mk(0, 0, 0);
       if (tr) {
@@ -905,7 +908,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (nsh == 0 || (ntr != 0 && nsh * RT_SHADE_DEN < (nsh + ntr) * RT_SHADE_NUM)) continue;
 
     const bool hit = state == S_SHADE;
-    c_shaded += nsh;
+    if (hit) cnt_add(CNT_SHADED, 1);
     // ComputeSurfaceProps (raytracer.go:106-122, 182-194, 242-260, 339-370)
     d3 pw = mk(0, 0, 0), nw = mk(0, 0, 1);
     int mat = 0;
@@ -971,7 +974,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         surf_bad = bad;
       }
     }
-    c_surferr += popc_ballot(surf_bad);
+    if (surf_bad) cnt_add(CNT_SURFERR, 1);
 
     // computeLighting + inShadow (raytracer.go:372-429)
     PH_MARK(3);
@@ -985,7 +988,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       d3 lth = sub(mk(lt[0], lt[1], lt[2]), pw);
       double dist = len(lth);
       d3 ldir = norm(lth);
-      c_shadow += nsh;
       bool open = hit;  // lanes still looking for an occluder
       Ray sr;
       sr.o = sorig;
@@ -994,19 +996,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       const float sslack = ray_slack(sof);
       // occluders must lie within t < dist / |ray.d| (raytracer.go:424)
       const float stmax = (float)(dist / rlen) * 1.0001f + 1e-4f;
+      // inShadow's test count is #{i < end, i != hit} with end = first
+      // occluder + 1 (or nobj); counted per kind from the prefix table below.
+      int send = P.nobj;
       if constexpr (!BVH) {
         for (int i = 0; i < P.nobj; i++) {
           if (!__any(open)) break;
           const int k = S.kind[i];
           const double* g = S.geo + (size_t)i * GEO;
           bool test = open && i != hit_i;
-          {
-            const uint64_t n = popc_ballot(test);
-            c_st0 += k == 0 ? n : 0;
-            c_st1 += k == 1 ? n : 0;
-            c_st2 += k == 2 ? n : 0;
-            c_st3 += k == 3 ? n : 0;
-          }
 #if RT_CULL
           test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
                                         : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
@@ -1016,7 +1014,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             double t;
             int f;
             if (object_hit(k, g, sr, t, f)) {
-              if (t * rlen < dist) open = false;
+              if (t * rlen < dist) {
+                open = false;
+                send = i + 1;
+              }
             }
           }
         }
@@ -1081,15 +1082,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           }
         }
         open = hit && occ == 0x7fffffff;
-        if (hit) {
-          const int end = occ == 0x7fffffff ? P.nobj : occ + 1;
-          const uint4 pe = *reinterpret_cast<const uint4*>(P.pref + (size_t)end * 4);
-          const int hk = hit_i < end ? S.kind[hit_i] : -1;
-          l_st0 += pe.x - (hk == 0 ? 1u : 0u);
-          l_st1 += pe.y - (hk == 1 ? 1u : 0u);
-          l_st2 += pe.z - (hk == 2 ? 1u : 0u);
-          l_st3 += pe.w - (hk == 3 ? 1u : 0u);
-        }
+        send = open ? P.nobj : occ + 1;
+      }
+      if (hit) {
+        const uint4 pe = *reinterpret_cast<const uint4*>(P.pref + (size_t)send * 4);
+        const int hk = hit_i < send ? S.kind[hit_i] : -1;
+        if (P.kind_mask & 1) cnt_add(CNT_ST0 + 0, pe.x - (hk == 0 ? 1u : 0u));
+        if (P.kind_mask & 2) cnt_add(CNT_ST0 + 1, pe.y - (hk == 1 ? 1u : 0u));
+        if (P.kind_mask & 4) cnt_add(CNT_ST0 + 2, pe.z - (hk == 2 ? 1u : 0u));
+        if (P.kind_mask & 8) cnt_add(CNT_ST0 + 3, pe.w - (hk == 3 ? 1u : 0u));
       }
       PH_MARK(4);
       if (hit && open) {
@@ -1203,20 +1204,18 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     atomicAdd(P.stats + ST_BVHDIAG + 4, (unsigned long long)bd_trays);
     atomicAdd(P.stats + ST_BVHDIAG + 5, (unsigned long long)bd_srays);
 #endif
-    atomicAdd(P.stats + ST_TRACED, (unsigned long long)c_traced);
-    atomicAdd(P.stats + ST_SHADOW, (unsigned long long)c_shadow);
-    atomicAdd(P.stats + ST_SHADED, (unsigned long long)c_shaded);
-    atomicAdd(P.stats + ST_SURFERR, (unsigned long long)c_surferr);
-    atomicAdd(P.stats + ST_STESTS + 0, (unsigned long long)c_st0);
-    atomicAdd(P.stats + ST_STESTS + 1, (unsigned long long)c_st1);
-    atomicAdd(P.stats + ST_STESTS + 2, (unsigned long long)c_st2);
-    atomicAdd(P.stats + ST_STESTS + 3, (unsigned long long)c_st3);
   }
-  if constexpr (BVH) {
-    atomicAdd(P.stats + ST_STESTS + 0, (unsigned long long)l_st0);
-    atomicAdd(P.stats + ST_STESTS + 1, (unsigned long long)l_st1);
-    atomicAdd(P.stats + ST_STESTS + 2, (unsigned long long)l_st2);
-    atomicAdd(P.stats + ST_STESTS + 3, (unsigned long long)l_st3);
+  // Workgroup reduction of the per-lane counters (every wave of the group
+  // leaves the main loop, so all reach the barrier).
+  __syncthreads();
+  if (threadIdx.x < NCNT) {
+    unsigned long long sum = 0;
+    for (int j = 0; j < WG; j++) sum += cnt[threadIdx.x * WG + j];
+    const int k = (int)threadIdx.x;
+    const int slot = k == CNT_TRACED ? ST_TRACED : (k == CNT_SHADED ? ST_SHADED : (k == CNT_SURFERR ? ST_SURFERR : ST_STESTS + (k - CNT_ST0)));
+    if (sum) atomicAdd(P.stats + slot, sum);
+    // one inShadow call per (shaded hit, light)
+    if (k == CNT_SHADED && sum) atomicAdd(P.stats + ST_SHADOW, sum * (unsigned long long)P.nlights);
   }
 }
 
@@ -1397,7 +1396,7 @@ struct DevScene {
   // BVH flavour: one device buffer nodes | leaf objects | planes | prefix counts
   char* accel = nullptr;
   bool use_bvh = false;
-  int nplanes = 0, nnodes = 0;
+  int nplanes = 0, nnodes = 0, kind_mask = 0;
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_pref = 0;
 };
 
@@ -1823,41 +1822,45 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   }
   s.kinds = kind;
   {
-    // Acceleration structure for scenes with many bounded objects.
+    // Acceleration buffer: [BVH nodes | leaf objects] | planes | per-kind
+    // prefix counts (shadow-test counters, both flavours).
     std::vector<int> bounded, planes;
     for (int i = 0; i < s.nobj; i++) (kind[i] == RT_PLANE ? planes : bounded).push_back(i);
+    BvhBuild b;
     if ((int)bounded.size() >= RT_BVH_MIN) {
-      BvhBuild b;
       b.c = &bcen;
       b.r = &brad;
       b.ord = bounded;
       b.alloc();
       b.build(0, 0, (int)bounded.size(), 0);
-      if (b.max_depth + 2 < BVH_STACK) {
-        std::vector<uint32_t> pref((size_t)(s.nobj + 1) * 4, 0u);
-        for (int i = 0; i < s.nobj; i++) {
-          for (int k = 0; k < 4; k++) pref[(size_t)(i + 1) * 4 + k] = pref[(size_t)i * 4 + k];
-          pref[(size_t)(i + 1) * 4 + kind[i]]++;
-        }
-        s.off_nodes = 0;
-        s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
-        s.off_planes = s.off_bobj + ((b.ord.size() * sizeof(int) + 15) & ~(size_t)15);
-        s.off_pref = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
-        std::vector<char> acc(s.off_pref + pref.size() * sizeof(uint32_t), 0);
-        std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
-        std::memcpy(acc.data() + s.off_bobj, b.ord.data(), b.ord.size() * sizeof(int));
-        if (!planes.empty()) std::memcpy(acc.data() + s.off_planes, planes.data(), planes.size() * sizeof(int));
-        std::memcpy(acc.data() + s.off_pref, pref.data(), pref.size() * sizeof(uint32_t));
-        int rc = upload(&s.accel, acc);
-        if (rc != RT_OK) {
-          free_scene(s);
-          return rc;
-        }
-        s.use_bvh = true;
-        s.nplanes = (int)planes.size();
-        s.nnodes = (int)(b.nodes.size() / BN);
-      }
+      s.use_bvh = b.max_depth + 2 < BVH_STACK;
     }
+    if (!s.use_bvh) {
+      b.nodes.clear();
+      b.ord.clear();
+    }
+    std::vector<uint32_t> pref((size_t)(s.nobj + 1) * 4, 0u);
+    for (int i = 0; i < s.nobj; i++) {
+      for (int k = 0; k < 4; k++) pref[(size_t)(i + 1) * 4 + k] = pref[(size_t)i * 4 + k];
+      pref[(size_t)(i + 1) * 4 + kind[i]]++;
+      s.kind_mask |= 1 << kind[i];
+    }
+    s.off_nodes = 0;
+    s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
+    s.off_planes = s.off_bobj + ((b.ord.size() * sizeof(int) + 15) & ~(size_t)15);
+    s.off_pref = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
+    std::vector<char> acc(s.off_pref + pref.size() * sizeof(uint32_t), 0);
+    if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
+    if (!b.ord.empty()) std::memcpy(acc.data() + s.off_bobj, b.ord.data(), b.ord.size() * sizeof(int));
+    if (!planes.empty()) std::memcpy(acc.data() + s.off_planes, planes.data(), planes.size() * sizeof(int));
+    std::memcpy(acc.data() + s.off_pref, pref.data(), pref.size() * sizeof(uint32_t));
+    int rc = upload(&s.accel, acc);
+    if (rc != RT_OK) {
+      free_scene(s);
+      return rc;
+    }
+    s.nplanes = (int)planes.size();
+    s.nnodes = (int)(b.nodes.size() / BN);
   }
   // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
   int frames = std::max(1, s.depth - 1);
@@ -1903,7 +1906,8 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int frames_off = lds ? s.blob_bytes : 0;
   const int vm_off = frames_off + WAVES_PER_WG * RT_LDS_FRAMES * CORE * 64 * (int)sizeof(double);
   const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
-  const int shmem = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * (int)sizeof(int) : 0);
+  const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * (int)sizeof(int) : 0);
+  const int shmem = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
   const void* kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true> : (const void*)rt_render_kernel<true, false>)
                         : (s.use_bvh ? (const void*)rt_render_kernel<false, true> : (const void*)rt_render_kernel<false, false>);
   int per_cu = 0;
@@ -1947,11 +1951,13 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     return fail(RT_E_INVALID, "image too large for one launch");
   P.total_slots = (unsigned int)slots;
   P.frames = std::max(1, s.depth - 1);
+  P.pref = reinterpret_cast<const uint32_t*>(s.accel + s.off_pref);
+  P.kind_mask = s.kind_mask;
+  P.cnt_off = cnt_off;
   if (s.use_bvh) {
     P.bvh_nodes = reinterpret_cast<const float*>(s.accel + s.off_nodes);
     P.bvh_obj = reinterpret_cast<const int*>(s.accel + s.off_bobj);
     P.planes = reinterpret_cast<const int*>(s.accel + s.off_planes);
-    P.pref = reinterpret_cast<const uint32_t*>(s.accel + s.off_pref);
     P.nplanes = s.nplanes;
     P.bvh_stack_off = stack_off;
   }
