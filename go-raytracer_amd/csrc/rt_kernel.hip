@@ -83,7 +83,10 @@ using namespace rt;
 // lights [nl][LGT]    0..2 position, 3..5 colour
 // kind   [nobj] int32;  objmat [nobj][OMAT] int32 per-face material index
 // ---------------------------------------------------------------------------
-enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8 };
+enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8, GLOB = 16 };
+// GLOB record (head of the lights section): 0..2 ambient, 3..5 bg start,
+// 6..8 bg end, 9 viewport width, 10 viewport height (read where used, so they
+// do not occupy scalar registers across the whole kernel)
 // Frame of one traceRay activation that has children (post-order combine).
 // Global layout: 14 fields, lane-interleaved: Lw[3] cfirst[3] pend_o[3]
 // pend_d[3] kr packed. The CORE fields (Lw, kr, packed) of the first
@@ -112,8 +115,6 @@ struct Params {
   int trow0, trow_stride;  // trow_stride > 0: output tile row j renders image tile row trow0 + j*stride
   unsigned int total_slots;
   int frames;  // stack frames per lane (depth - 1, >= 1)
-  double vw, vh;
-  double amb[3], bg0[3], bg1[3];
   // BVH flavour (scenes with many bounded objects)
   const float* bvh_nodes;  // [n][BN]: lo xyz, hi xyz, then int first, count, minidx, axis
   const int* bvh_obj;      // leaf object indices (ascending within a leaf)
@@ -580,7 +581,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   S.geo = reinterpret_cast<const double*>(base + P.off_geo);
   S.shade = reinterpret_cast<const double*>(base + P.off_shade);
   S.mats = reinterpret_cast<const double*>(base + P.off_mats);
-  S.lights = reinterpret_cast<const double*>(base + P.off_lights);
+  // lights section: a 16-double record of per-frame constants, then the lights
+  const double* G = reinterpret_cast<const double*>(base + P.off_lights);
+  S.lights = G + GLOB;
   S.kind = reinterpret_cast<const int*>(base + P.off_kind);
   S.objmat = reinterpret_cast<const int*>(base + P.off_objmat);
   S.code = reinterpret_cast<const uint32_t*>(base + P.off_code);
@@ -645,8 +648,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   auto gen_ray = [&]() {
     double dx = pcg_float64(rng) - 0.5;
     double dy = pcg_float64(rng) - 0.5;
-    double u = ((double)px + dx) / W1 * P.vw - P.vw / 2.0;
-    double v = ((double)py + dy) / H1 * P.vh - P.vh / 2.0;
+    const double vw = G[9], vh = G[10];
+    double u = ((double)px + dx) / W1 * vw - vw / 2.0;
+    double v = ((double)py + dy) / H1 * vh - vh / 2.0;
     ray.o = mk(u, -v, 0.0);
     ray.d = norm(sub(ray.o, eye));
   };
@@ -895,7 +899,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           hit_t = best_t;
         } else {  // background gradient, raytracer.go:493-497
           double t = 0.5 * (ray.d.y + 1.0);
-          res = lerp(mk(P.bg0[0], P.bg0[1], P.bg0[2]), mk(P.bg1[0], P.bg1[1], P.bg1[2]), t);
+          res = lerp(mk(G[3], G[4], G[5]), mk(G[6], G[7], G[8]), t);
         }
       }
       unwind(tr && !found, res, pf, pf_packed, pf_lw, pf_kr);
@@ -980,7 +984,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     PH_MARK(3);
     const double* M = mat >= 0 ? S.mats + (size_t)mat * MAT : vmrec;
     d3 L = mk(0, 0, 0);
-    if (hit) L = scale(mk(P.amb[0], P.amb[1], P.amb[2]), M[9]);
+    if (hit) L = scale(mk(G[0], G[1], G[2]), M[9]);
     const double rlen = len(ray.d);
     const d3 sorig = add(pw, scale(nw, 1e-4));
     for (int li = 0; li < P.nlights; li++) {
@@ -1751,11 +1755,18 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     d[10] = mm.ks;
     d[11] = mm.specular_exponent;
   }
-  std::vector<double> lights((size_t)std::max(1, s.nlights) * LGT, 0.0);
+  std::vector<double> lights(GLOB + (size_t)std::max(1, s.nlights) * LGT, 0.0);
+  for (int k = 0; k < 3; k++) {
+    lights[k] = s.amb[k];
+    lights[3 + k] = s.bg0[k];
+    lights[6 + k] = s.bg1[k];
+  }
+  lights[9] = s.vw;
+  lights[10] = s.vh;
   for (int l = 0; l < s.nlights; l++)
     for (int k = 0; k < 3; k++) {
-      lights[(size_t)l * LGT + k] = in->lights[l].position[k];
-      lights[(size_t)l * LGT + 3 + k] = in->lights[l].color[k];
+      lights[GLOB + (size_t)l * LGT + k] = in->lights[l].position[k];
+      lights[GLOB + (size_t)l * LGT + 3 + k] = in->lights[l].color[k];
     }
   // One blob: geo | shade | mats | lights | kind | objmat (16-B aligned sections).
   s.off_geo = 0;
@@ -1961,13 +1972,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     P.nplanes = s.nplanes;
     P.bvh_stack_off = stack_off;
   }
-  P.vw = s.vw;
-  P.vh = s.vh;
-  for (int k = 0; k < 3; k++) {
-    P.amb[k] = s.amb[k];
-    P.bg0[k] = s.bg0[k];
-    P.bg1[k] = s.bg1[k];
-  }
+
   HIP_TRY(hipMemsetAsync(c->queue, 0, 256, st));
   HIP_TRY(hipEventRecord(c->ev0, st));
   const char* blob = s.blob;
