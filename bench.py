@@ -104,18 +104,20 @@ def main():
     torch.cuda.synchronize()
     ctx.read_stats(reset=True)
 
-    kernel_ms = []
+    # Kernel time: torch events on the launch stream around each render launch
+    # inside the timed region, read after it (no host sync per step).
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dr.step()
-        if dr.has_work():
-            kernel_ms.append(ctx.last_kernel_ms())
+    for k in range(args.steps):
+        dr.step(events=evs[k])
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    kernel_ms = [e0.elapsed_time(e1) for e0, e1 in evs] if dr.has_work() else []
     st = ctx.read_stats(reset=True)
 
     rays_local = st.total_rays()

@@ -87,13 +87,20 @@ class DistributedRenderer:
     def has_work(self):
         return self.ntrows > 0 if self.mode == "interleaved" else self.y1 > self.y0
 
-    def step(self, gather=True):
+    def step(self, gather=True, events=None):
+        """Render this rank's rows and gather the frame. `events` (start, end):
+        torch.cuda.Events recorded on the launch stream around the render
+        kernel, for kernel timing without a host sync per step."""
+        if events is not None:
+            events[0].record()
         if self.mode == "interleaved":
             if self.ntrows > 0:
                 self.ctx.render_tile_rows_async(self.rank, self.world, self.ntrows,
                                                 self.buf[: self.ntrows * TILE])
         elif self.y1 > self.y0:
             self.ctx.render_rows_async(self.y0, self.y1, self.buf[: self.y1 - self.y0])
+        if events is not None:
+            events[1].record()
         if gather:
             self.frame = gather_frame(self.buf, self.H, self.mode)
         return self.frame
