@@ -116,8 +116,8 @@ struct Params {
   unsigned int total_slots;
   int frames;  // stack frames per lane (depth - 1, >= 1)
   // BVH flavour (scenes with many bounded objects)
-  const float* bvh_nodes;  // [n][BN]: lo xyz, hi xyz, then int first, count, minidx, axis
-  const int* bvh_obj;      // leaf object indices (ascending within a leaf)
+  const float* bvh_nodes;  // internal nodes [n][BN] (see BvhBuild)
+  const double* bvh_geo;   // leaf objects in BVH order: geo record, 14 = index, 15 = kind
   const int* planes;       // unbounded objects, ascending index
   const uint32_t* pref;    // [nobj + 1][4]: objects of each kind with index < i
   int nplanes, bvh_stack_off;
@@ -128,7 +128,11 @@ struct Params {
 // workgroup at exit: per-wave 64-bit SGPR counters pushed the kernel into
 // SGPR spilling (C2 +33% time, C3 +7%).
 enum { CNT_TRACED = 0, CNT_SHADED = 1, CNT_SURFERR = 2, CNT_ST0 = 3, NCNT = 7 };
-enum { BN = 12, BVH_STACK = 64 };
+// BVH node: child 0 box (lo xyz, hi xyz), child 1 box, then as int: ref 0,
+// ref 1, smallest object index under child 0, under child 1. A ref is
+// (node << 3) for an internal node, (first << 3) | count for a leaf of
+// `count` (1..4) consecutive bvh_geo records.
+enum { BN = 16, BVH_STACK = 64 };
 
 struct Ray {
   d3 o, d;
@@ -356,14 +360,26 @@ __device__ __forceinline__ float ray_slack(F3 o) {
 // component 0 * inf = NaN is ignored by fminf/fmaxf, i.e. a ray parallel to a
 // slab is constrained only by the other axes (it lies on or beyond the
 // widened face otherwise).
-__device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax, const float* nb) {
+__device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax, const float* nb, float& tn) {
   const float x0 = (nb[0] - slack - o.x) * id.x, x1 = (nb[3] + slack - o.x) * id.x;
   const float y0 = (nb[1] - slack - o.y) * id.y, y1 = (nb[4] + slack - o.y) * id.y;
   const float z0 = (nb[2] - slack - o.z) * id.z, z1 = (nb[5] + slack - o.z) * id.z;
-  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
   const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
   return tn <= tf && tf >= 0.0f && tn <= tmax;
 }
+// Per-wave traversal stack in LDS: node refs and the lanes still active there.
+struct WaveStack {
+  int* ref;
+  uint64_t* mask;
+  __device__ __forceinline__ void push(int& sp, int lane, int r, uint64_t m) {
+    if (lane == 0) {
+      ref[sp] = r;
+      mask[sp] = m;
+    }
+    sp++;
+  }
+};
 __device__ __forceinline__ F3 f3_rcp(F3 d) {
   return F3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
 }
@@ -633,7 +649,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off);
   for (int k = 0; k < NCNT; k++) cnt[k * WG + threadIdx.x] = 0;
   auto cnt_add = [&](int k, uint64_t v) { atomicAdd(&cnt[k * WG + threadIdx.x], (unsigned long long)v); };
-  int* bstk = reinterpret_cast<int*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
+  WaveStack bst;
+  bst.mask = reinterpret_cast<uint64_t*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
+  bst.ref = reinterpret_cast<int*>(smem + P.bvh_stack_off + WAVES_PER_WG * BVH_STACK * 8) + (threadIdx.x >> 6) * BVH_STACK;
 #ifdef RT_PHASE_TIMING
   uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t bd_tnodes = 0, bd_snodes = 0, bd_tleaf = 0, bd_sleaf = 0, bd_trays = 0, bd_srays = 0;
@@ -819,9 +837,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       // The linear loop visits objects in index order (strict <, the first
       // index wins ties); the BVH visits them in any order and breaks ties on
       // the index explicitly, which selects the same object.
-      auto trace_obj = [&](int i, bool act) {
-        const int k = S.kind[i];
-        const double* g = S.geo + (size_t)i * GEO;
+      auto trace_obj = [&](int i, int k, const double* g, bool act) {
         bool test = act;
 #if RT_CULL
         // an object entered beyond the lane's current best cannot win (strict <)
@@ -844,47 +860,57 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         }
       };
       if constexpr (!BVH) {
-        for (int i = 0; i < P.nobj; i++) trace_obj(i, tr);
+        for (int i = 0; i < P.nobj; i++) trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
       } else {
-        for (int p = 0; p < P.nplanes; p++) trace_obj(P.planes[p], tr);
+        for (int p = 0; p < P.nplanes; p++) {
+          const int i = P.planes[p];
+          trace_obj(i, RT_PLANE, S.geo + (size_t)i * GEO, tr);
+        }
         const F3 idf = f3_rcp(df);
 #ifdef RT_PHASE_TIMING
         bd_trays++;
 #endif
-        int ssp = 1;
-        if (lane == 0) bstk[0] = 0;
+        int ssp = 0;
+        bst.push(ssp, lane, 0, __ballot(tr));
         while (ssp > 0) {
           ssp--;
-          const int node = __builtin_amdgcn_readfirstlane(bstk[ssp]);
-          const float* nb = P.bvh_nodes + (size_t)node * BN;
-          const int* ni = reinterpret_cast<const int*>(nb + 6);
-          const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
-          const bool act = tr && may_hit_box(of, idf, slack, tmax, nb);
-          const uint64_t am = __ballot(act);
+          const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
+          const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+          const bool act = tr && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
           bd_tnodes++;
 #ifdef RT_COST_MAP
           if (tr) lane_cost++;
 #endif
 #endif
-          if (am == 0) continue;
-          const int first = ni[0], count = ni[1];
-          if (count > 0) {
+          if (r & 7) {  // leaf
 #ifdef RT_PHASE_TIMING
             bd_tleaf++;
 #endif
-            for (int j = first; j < first + count; j++) trace_obj(P.bvh_obj[j], act);
-          } else {
-            // near child first: the side most active lanes travel from
-            const int axis = ni[3];
-            const float da = axis == 0 ? df.x : (axis == 1 ? df.y : df.z);
-            const uint64_t neg = __ballot(act && da < 0.0f);
-            const bool hi_first = 2 * __popcll(neg) > __popcll(am);
-            if (lane == 0) {
-              bstk[ssp] = hi_first ? first : first + 1;
-              bstk[ssp + 1] = hi_first ? first + 1 : first;
+            const int first = r >> 3, count = r & 7;
+            for (int j = first; j < first + count; j++) {
+              const double* g = P.bvh_geo + (size_t)j * GEO;
+              const int* gi = reinterpret_cast<const int*>(g + 14);
+              trace_obj(gi[0], gi[2], g, act);
             }
-            ssp += 2;
+          } else {
+            const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
+            const int* ni = reinterpret_cast<const int*>(nb + 12);
+            const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+            float t0, t1;
+            const bool a0 = act && may_hit_box(of, idf, slack, tmax, nb, t0);
+            const bool a1 = act && may_hit_box(of, idf, slack, tmax, nb + 6, t1);
+            const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+            // near child popped first: the one most lanes enter first
+            const bool c1_first = 2 * __popcll(__ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
+            if (c1_first) {
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+            } else {
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+            }
           }
         }
       }
@@ -1032,9 +1058,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         // lower than the best so far) and derives the count from prefix
         // counts per kind. The shadow verdict is the same either way.
         int occ = 0x7fffffff;
-        auto shadow_obj = [&](int i, bool act) {
-          const int k = S.kind[i];
-          const double* g = S.geo + (size_t)i * GEO;
+        auto shadow_obj = [&](int i, int k, const double* g, bool act) {
           bool test = act && i != hit_i && i < occ;
           test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
                                         : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
@@ -1047,42 +1071,53 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             }
           }
         };
-        for (int p = 0; p < P.nplanes; p++) shadow_obj(P.planes[p], hit);
+        for (int p = 0; p < P.nplanes; p++) {
+          const int i = P.planes[p];
+          shadow_obj(i, RT_PLANE, S.geo + (size_t)i * GEO, hit);
+        }
         const F3 sidf = f3_rcp(sdf);
 #ifdef RT_PHASE_TIMING
         bd_srays++;
 #endif
-        int ssp = 1;
-        if (lane == 0) bstk[0] = 0;
+        int ssp = 0;
+        bst.push(ssp, lane, 0, __ballot(hit));
         while (ssp > 0) {
           ssp--;
-          const int node = __builtin_amdgcn_readfirstlane(bstk[ssp]);
-          const float* nb = P.bvh_nodes + (size_t)node * BN;
-          const int* ni = reinterpret_cast<const int*>(nb + 6);
-          const bool act = hit && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb);
+          const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
+          const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+          const bool act = hit && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
           bd_snodes++;
 #ifdef RT_COST_MAP
           if (hit) lane_cost++;
 #endif
 #endif
-          if (!__any(act)) continue;
-          const int first = ni[0], count = ni[1];
-          if (count > 0) {
+          if (r & 7) {  // leaf
 #ifdef RT_PHASE_TIMING
             bd_sleaf++;
 #endif
-            for (int j = first; j < first + count; j++) shadow_obj(P.bvh_obj[j], act);
-          } else {
-            // lower-index subtree first: it can prune the other
-            const int* li = reinterpret_cast<const int*>(P.bvh_nodes + (size_t)first * BN + 6);
-            const int* ri = reinterpret_cast<const int*>(P.bvh_nodes + (size_t)(first + 1) * BN + 6);
-            const bool right_first = ri[2] < li[2];
-            if (lane == 0) {
-              bstk[ssp] = right_first ? first : first + 1;
-              bstk[ssp + 1] = right_first ? first + 1 : first;
+            const int first = r >> 3, count = r & 7;
+            for (int j = first; j < first + count; j++) {
+              const double* g = P.bvh_geo + (size_t)j * GEO;
+              const int* gi = reinterpret_cast<const int*>(g + 14);
+              shadow_obj(gi[0], gi[2], g, act);
             }
-            ssp += 2;
+          } else {
+            const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
+            const int* ni = reinterpret_cast<const int*>(nb + 12);
+            float t0, t1;
+            const bool a0 = act && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb, t0);
+            const bool a1 = act && ni[3] < occ && may_hit_box(sof, sidf, sslack, stmax, nb + 6, t1);
+            const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+            // lower-index subtree popped first: it can prune the other
+            if (ni[3] < ni[2]) {
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+            } else {
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+            }
           }
         }
         open = hit && occ == 0x7fffffff;
@@ -1421,26 +1456,31 @@ float f_up(double x) {
 // Median-split BVH over the bounded objects' padded bounding spheres (boxes
 // rounded outwards to FP32). Median splits keep the depth at ~log2(n / 4), far
 // below the device stack (BVH_STACK entries); leaves hold <= 4 objects in
-// ascending index order.
+// ascending index order, copied (geo record + index + kind) into leaf order.
 struct BvhBuild {
   const std::vector<double>* c;  // [n][3] centres
   const std::vector<double>* r;  // [n] radii
+  const std::vector<double>* geo;
+  const std::vector<int>* kind;
   std::vector<int> ord;          // object indices
   std::vector<float> nodes;      // [m][BN]
+  std::vector<double> leaf_geo;  // [n][GEO] in leaf order
   int max_depth = 0;
 
-  int alloc() {
-    nodes.resize(nodes.size() + BN, 0.0f);
-    return (int)(nodes.size() / BN) - 1;
-  }
-  void build(int node, int lo, int hi, int depth) {
+  struct Sub {
+    int ref;
+    float box[6];
+    int minidx;
+  };
+  Sub build(int lo, int hi, int depth) {
     max_depth = std::max(max_depth, depth);
+    Sub out;
     double bl[3] = {1e300, 1e300, 1e300}, bh[3] = {-1e300, -1e300, -1e300};
     double cl[3] = {1e300, 1e300, 1e300}, ch[3] = {-1e300, -1e300, -1e300};
-    int minidx = 0x7fffffff;
+    out.minidx = 0x7fffffff;
     for (int j = lo; j < hi; j++) {
       const int i = ord[j];
-      minidx = std::min(minidx, i);
+      out.minidx = std::min(out.minidx, i);
       for (int k = 0; k < 3; k++) {
         const double cc = (*c)[(size_t)i * 3 + k], rr = (*r)[i];
         bl[k] = std::min(bl[k], cc - rr);
@@ -1449,19 +1489,24 @@ struct BvhBuild {
         ch[k] = std::max(ch[k], cc);
       }
     }
-    float* nb = &nodes[(size_t)node * BN];
     for (int k = 0; k < 3; k++) {
-      nb[k] = f_down(bl[k]);
-      nb[3 + k] = f_up(bh[k]);
+      out.box[k] = f_down(bl[k]);
+      out.box[3 + k] = f_up(bh[k]);
     }
-    int* ni = reinterpret_cast<int*>(nb + 6);
-    ni[2] = minidx;
     if (hi - lo <= 4) {
       std::sort(ord.begin() + lo, ord.begin() + hi);
-      ni[0] = lo;
-      ni[1] = hi - lo;
-      ni[3] = 0;
-      return;
+      const int first = (int)(leaf_geo.size() / GEO);
+      for (int j = lo; j < hi; j++) {
+        const int i = ord[j];
+        leaf_geo.insert(leaf_geo.end(), geo->begin() + (size_t)i * GEO, geo->begin() + (size_t)(i + 1) * GEO);
+        int* gi = reinterpret_cast<int*>(&leaf_geo[leaf_geo.size() - GEO + 14]);
+        gi[0] = i;
+        gi[1] = 0;
+        gi[2] = (*kind)[i];
+        gi[3] = 0;
+      }
+      out.ref = (first << 3) | (hi - lo);
+      return out;
     }
     int axis = 0;
     for (int k = 1; k < 3; k++)
@@ -1471,15 +1516,22 @@ struct BvhBuild {
       const double ca = (*c)[(size_t)a * 3 + axis], cb = (*c)[(size_t)b * 3 + axis];
       return ca < cb || (ca == cb && a < b);
     });
-    const int left = alloc();
-    alloc();
-    nb = &nodes[(size_t)node * BN];  // alloc may have moved the storage
-    ni = reinterpret_cast<int*>(nb + 6);
-    ni[0] = left;
-    ni[1] = 0;
-    ni[3] = axis;
-    build(left, lo, mid, depth + 1);
-    build(left + 1, mid, hi, depth + 1);
+    const int node = (int)(nodes.size() / BN);
+    nodes.resize(nodes.size() + BN, 0.0f);
+    const Sub l = build(lo, mid, depth + 1);
+    const Sub rr = build(mid, hi, depth + 1);
+    float* nb = &nodes[(size_t)node * BN];
+    for (int k = 0; k < 6; k++) {
+      nb[k] = l.box[k];
+      nb[6 + k] = rr.box[k];
+    }
+    int* ni = reinterpret_cast<int*>(nb + 12);
+    ni[0] = l.ref;
+    ni[1] = rr.ref;
+    ni[2] = l.minidx;
+    ni[3] = rr.minidx;
+    out.ref = node << 3;
+    return out;
   }
 };
 
@@ -1841,14 +1893,15 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     if ((int)bounded.size() >= RT_BVH_MIN) {
       b.c = &bcen;
       b.r = &brad;
+      b.geo = &geo;
+      b.kind = &kind;
       b.ord = bounded;
-      b.alloc();
-      b.build(0, 0, (int)bounded.size(), 0);
+      b.build(0, (int)bounded.size(), 0);  // root: node 0 (> 4 objects)
       s.use_bvh = b.max_depth + 2 < BVH_STACK;
     }
     if (!s.use_bvh) {
       b.nodes.clear();
-      b.ord.clear();
+      b.leaf_geo.clear();
     }
     std::vector<uint32_t> pref((size_t)(s.nobj + 1) * 4, 0u);
     for (int i = 0; i < s.nobj; i++) {
@@ -1858,11 +1911,12 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     }
     s.off_nodes = 0;
     s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
-    s.off_planes = s.off_bobj + ((b.ord.size() * sizeof(int) + 15) & ~(size_t)15);
+    s.off_planes = s.off_bobj + ((b.leaf_geo.size() * sizeof(double) + 15) & ~(size_t)15);
     s.off_pref = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
     std::vector<char> acc(s.off_pref + pref.size() * sizeof(uint32_t), 0);
     if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
-    if (!b.ord.empty()) std::memcpy(acc.data() + s.off_bobj, b.ord.data(), b.ord.size() * sizeof(int));
+    if (!b.leaf_geo.empty())
+      std::memcpy(acc.data() + s.off_bobj, b.leaf_geo.data(), b.leaf_geo.size() * sizeof(double));
     if (!planes.empty()) std::memcpy(acc.data() + s.off_planes, planes.data(), planes.size() * sizeof(int));
     std::memcpy(acc.data() + s.off_pref, pref.data(), pref.size() * sizeof(uint32_t));
     int rc = upload(&s.accel, acc);
@@ -1917,7 +1971,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int frames_off = lds ? s.blob_bytes : 0;
   const int vm_off = frames_off + WAVES_PER_WG * RT_LDS_FRAMES * CORE * 64 * (int)sizeof(double);
   const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
-  const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * (int)sizeof(int) : 0);
+  const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * 12 : 0);
   const int shmem = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
   const void* kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true> : (const void*)rt_render_kernel<true, false>)
                         : (s.use_bvh ? (const void*)rt_render_kernel<false, true> : (const void*)rt_render_kernel<false, false>);
@@ -1967,7 +2021,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.cnt_off = cnt_off;
   if (s.use_bvh) {
     P.bvh_nodes = reinterpret_cast<const float*>(s.accel + s.off_nodes);
-    P.bvh_obj = reinterpret_cast<const int*>(s.accel + s.off_bobj);
+    P.bvh_geo = reinterpret_cast<const double*>(s.accel + s.off_bobj);
     P.planes = reinterpret_cast<const int*>(s.accel + s.off_planes);
     P.nplanes = s.nplanes;
     P.bvh_stack_off = stack_off;

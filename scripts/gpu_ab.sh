@@ -1,5 +1,10 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-baseline off > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
-timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --cpu-baseline off > gpurun_out/bench_c2.json 2>> gpurun_out/bench.err || exit 1
+timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
+grep -q "pytest rc=0" gpurun_out/pytest_gpu.log || exit 1
+B=build_variants
+V="$B/librtamd_t_base.so go-raytracer_amd/csrc/librtamd.so"
+timeout -k 10 300 python scripts/ab.py --config c4 --rounds 7 $V > gpurun_out/ab_c4.log 2>&1 || exit 1
+timeout -k 10 300 python scripts/ab.py --config c5 --width 960 --height 540 --rounds 3 $V > gpurun_out/ab_c5.log 2>&1 || exit 1
+timeout -k 10 300 python scripts/ab.py --config c5 --width 960 --height 540 --rounds 1 $B/librtamd_phase.so > gpurun_out/phase_c5.log 2>&1 || exit 1
