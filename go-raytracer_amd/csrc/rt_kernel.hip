@@ -103,7 +103,8 @@ enum { LDS_MAX_BYTES = RT_LDS_MAX };
 
 struct Params {
   int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
-  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_code, off_consts, off_entry, blob_bytes;
+  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_code, off_consts, off_entry,
+      blob_bytes;
   int lds_vm_off;     // LDS byte offset of the per-lane VM material records (LDS flavour)
   double* vm_global;  // per-lane VM material records (global flavour)
   const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
@@ -119,7 +120,6 @@ struct Params {
   const float* bvh_nodes;  // internal nodes [n][BN] (see BvhBuild)
   const double* bvh_geo;   // leaf objects in BVH order: geo record, 14 = index, 15 = kind
   const int* planes;       // unbounded objects, ascending index
-  const uint32_t* pref;    // [nobj + 1][4]: objects of each kind with index < i
   int nplanes, bvh_stack_off;
   int cnt_off;    // LDS byte offset of the per-lane event counters [NCNT][WG]
   int kind_mask;  // bit k: the scene has objects of kind k
@@ -574,6 +574,7 @@ struct View {
   const double* lights;
   const int* kind;
   const int* objmat;
+  const uint32_t* pref;  // [nobj + 1][4]: objects of each kind with index < i
 };
 
 template <bool LDS, bool BVH>
@@ -602,6 +603,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   S.lights = G + GLOB;
   S.kind = reinterpret_cast<const int*>(base + P.off_kind);
   S.objmat = reinterpret_cast<const int*>(base + P.off_objmat);
+  S.pref = reinterpret_cast<const uint32_t*>(base + P.off_pref);
   S.code = reinterpret_cast<const uint32_t*>(base + P.off_code);
   S.entry = reinterpret_cast<const int*>(base + P.off_entry);
   S.consts = reinterpret_cast<const uint64_t*>(base + P.off_consts);
@@ -1013,6 +1015,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (hit) L = scale(mk(G[0], G[1], G[2]), M[9]);
     const double rlen = len(ray.d);
     const d3 sorig = add(pw, scale(nw, 1e-4));
+    uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind
     for (int li = 0; li < P.nlights; li++) {
       const double* lt = S.lights + (size_t)li * LGT;
       d3 lth = sub(mk(lt[0], lt[1], lt[2]), pw);
@@ -1124,12 +1127,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         send = open ? P.nobj : occ + 1;
       }
       if (hit) {
-        const uint4 pe = *reinterpret_cast<const uint4*>(P.pref + (size_t)send * 4);
+        const uint4 pe = *reinterpret_cast<const uint4*>(S.pref + (size_t)send * 4);
         const int hk = hit_i < send ? S.kind[hit_i] : -1;
-        if (P.kind_mask & 1) cnt_add(CNT_ST0 + 0, pe.x - (hk == 0 ? 1u : 0u));
-        if (P.kind_mask & 2) cnt_add(CNT_ST0 + 1, pe.y - (hk == 1 ? 1u : 0u));
-        if (P.kind_mask & 4) cnt_add(CNT_ST0 + 2, pe.z - (hk == 2 ? 1u : 0u));
-        if (P.kind_mask & 8) cnt_add(CNT_ST0 + 3, pe.w - (hk == 3 ? 1u : 0u));
+        sc0 += pe.x - (hk == 0 ? 1u : 0u);
+        sc1 += pe.y - (hk == 1 ? 1u : 0u);
+        sc2 += pe.z - (hk == 2 ? 1u : 0u);
+        sc3 += pe.w - (hk == 3 ? 1u : 0u);
       }
       PH_MARK(4);
       if (hit && open) {
@@ -1142,6 +1145,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         L = add(add(L, diffuse), specular);
       }
       PH_MARK(5);
+    }
+    if (hit) {
+      if (P.kind_mask & 1) cnt_add(CNT_ST0 + 0, sc0);
+      if (P.kind_mask & 2) cnt_add(CNT_ST0 + 1, sc1);
+      if (P.kind_mask & 4) cnt_add(CNT_ST0 + 2, sc2);
+      if (P.kind_mask & 8) cnt_add(CNT_ST0 + 3, sc3);
     }
 
     // traceRay body after lighting (raytracer.go:505-561)
@@ -1429,14 +1438,14 @@ struct DevScene {
   double amb[3] = {0, 0, 0}, bg0[3] = {0, 0, 0}, bg1[3] = {0, 0, 0};
   char* blob = nullptr;
   int blob_bytes = 0;
-  int off_geo = 0, off_shade = 0, off_mats = 0, off_lights = 0, off_kind = 0, off_objmat = 0;
+  int off_geo = 0, off_shade = 0, off_mats = 0, off_lights = 0, off_kind = 0, off_objmat = 0, off_prefb = 0;
   std::vector<int> kinds;  // host copy for the per-kind test counts
   int off_code = 0, off_consts = 0, off_entry = 0, num_programs = 0;
   // BVH flavour: one device buffer nodes | leaf objects | planes | prefix counts
   char* accel = nullptr;
   bool use_bvh = false;
   int nplanes = 0, nnodes = 0, kind_mask = 0;
-  size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_pref = 0;
+  size_t off_nodes = 0, off_bobj = 0, off_planes = 0;
 };
 
 // Scenes with at least this many bounded objects use the BVH flavour.
@@ -1860,7 +1869,14 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     }
   }
   s.num_programs = nprog;
-  s.off_code = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
+  // per-kind prefix counts (shadow-test counters)
+  std::vector<uint32_t> prefb((size_t)(s.nobj + 1) * 4, 0u);
+  for (int i = 0; i < s.nobj; i++) {
+    for (int k = 0; k < 4; k++) prefb[(size_t)(i + 1) * 4 + k] = prefb[(size_t)i * 4 + k];
+    prefb[(size_t)(i + 1) * 4 + kind[i]]++;
+  }
+  s.off_prefb = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
+  s.off_code = align16(s.off_prefb + (int)(prefb.size() * sizeof(uint32_t)));
   s.off_consts = align16(s.off_code + ncode * (int)sizeof(uint32_t));
   s.off_entry = align16(s.off_consts + nconst * (int)sizeof(uint64_t));
   s.blob_bytes = align16(s.off_entry + nprog * (int)sizeof(int));
@@ -1872,6 +1888,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     std::memcpy(blob.data() + s.off_lights, lights.data(), lights.size() * sizeof(double));
     std::memcpy(blob.data() + s.off_kind, kind.data(), kind.size() * sizeof(int));
     std::memcpy(blob.data() + s.off_objmat, objmat.data(), objmat.size() * sizeof(int));
+    std::memcpy(blob.data() + s.off_prefb, prefb.data(), prefb.size() * sizeof(uint32_t));
     if (nprog) {
       std::memcpy(blob.data() + s.off_code, in->program_code, (size_t)ncode * sizeof(uint32_t));
       std::memcpy(blob.data() + s.off_consts, in->program_consts, (size_t)nconst * sizeof(uint64_t));
@@ -1885,8 +1902,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   }
   s.kinds = kind;
   {
-    // Acceleration buffer: [BVH nodes | leaf objects] | planes | per-kind
-    // prefix counts (shadow-test counters, both flavours).
+    // Acceleration buffer: [BVH nodes | leaf objects] | planes.
     std::vector<int> bounded, planes;
     for (int i = 0; i < s.nobj; i++) (kind[i] == RT_PLANE ? planes : bounded).push_back(i);
     BvhBuild b;
@@ -1903,22 +1919,15 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       b.nodes.clear();
       b.leaf_geo.clear();
     }
-    std::vector<uint32_t> pref((size_t)(s.nobj + 1) * 4, 0u);
-    for (int i = 0; i < s.nobj; i++) {
-      for (int k = 0; k < 4; k++) pref[(size_t)(i + 1) * 4 + k] = pref[(size_t)i * 4 + k];
-      pref[(size_t)(i + 1) * 4 + kind[i]]++;
-      s.kind_mask |= 1 << kind[i];
-    }
+    for (int i = 0; i < s.nobj; i++) s.kind_mask |= 1 << kind[i];
     s.off_nodes = 0;
     s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
     s.off_planes = s.off_bobj + ((b.leaf_geo.size() * sizeof(double) + 15) & ~(size_t)15);
-    s.off_pref = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
-    std::vector<char> acc(s.off_pref + pref.size() * sizeof(uint32_t), 0);
+    std::vector<char> acc(s.off_planes + std::max<size_t>(1, planes.size()) * sizeof(int), 0);
     if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
     if (!b.leaf_geo.empty())
       std::memcpy(acc.data() + s.off_bobj, b.leaf_geo.data(), b.leaf_geo.size() * sizeof(double));
     if (!planes.empty()) std::memcpy(acc.data() + s.off_planes, planes.data(), planes.size() * sizeof(int));
-    std::memcpy(acc.data() + s.off_pref, pref.data(), pref.size() * sizeof(uint32_t));
     int rc = upload(&s.accel, acc);
     if (rc != RT_OK) {
       free_scene(s);
@@ -1989,6 +1998,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.off_lights = s.off_lights;
   P.off_kind = s.off_kind;
   P.off_objmat = s.off_objmat;
+  P.off_pref = s.off_prefb;
   P.off_code = s.off_code;
   P.off_consts = s.off_consts;
   P.off_entry = s.off_entry;
@@ -2016,7 +2026,6 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     return fail(RT_E_INVALID, "image too large for one launch");
   P.total_slots = (unsigned int)slots;
   P.frames = std::max(1, s.depth - 1);
-  P.pref = reinterpret_cast<const uint32_t*>(s.accel + s.off_pref);
   P.kind_mask = s.kind_mask;
   P.cnt_off = cnt_off;
   if (s.use_bvh) {

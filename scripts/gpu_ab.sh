@@ -5,6 +5,6 @@ timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.lo
 grep -q "pytest rc=0" gpurun_out/pytest_gpu.log || exit 1
 B=build_variants
 V="$B/librtamd_t_base.so go-raytracer_amd/csrc/librtamd.so"
-timeout -k 10 300 python scripts/ab.py --config c4 --rounds 7 $V > gpurun_out/ab_c4.log 2>&1 || exit 1
-timeout -k 10 300 python scripts/ab.py --config c5 --width 960 --height 540 --rounds 3 $V > gpurun_out/ab_c5.log 2>&1 || exit 1
-timeout -k 10 300 python scripts/ab.py --config c5 --width 960 --height 540 --rounds 1 $B/librtamd_phase.so > gpurun_out/phase_c5.log 2>&1 || exit 1
+for c in c3 c2 c4; do
+timeout -k 10 300 python scripts/ab.py --config $c --rounds 9 $V > gpurun_out/ab_$c.log 2>&1 || exit 1
+done
