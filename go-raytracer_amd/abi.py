@@ -5,16 +5,19 @@ sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
+RT_ABI_VERSION = 2  # include/rt_abi.h
+
 RT_OK = 0
 RT_E_INVALID = -1
 RT_E_SINGULAR = -2
 RT_E_DEVICE = -3
 RT_E_NOMEM = -4
 
-RT_SPHERE, RT_PLANE, RT_CUBE, RT_CYLINDER = 0, 1, 2, 3
-RT_NUM_KINDS = 4
+RT_SPHERE, RT_PLANE, RT_CUBE, RT_CYLINDER, RT_CONE = 0, 1, 2, 3, 4
+RT_NUM_KINDS = 5
 RT_MAX_FACES = 6
-KIND_NAMES = ("sphere", "plane", "cube", "cylinder")
+KIND_NAMES = ("sphere", "plane", "cube", "cylinder", "cone")
+RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_SPOT = 0, 1, 2
 
 
 class rt_material(C.Structure):
@@ -32,6 +35,18 @@ class rt_material(C.Structure):
 
 class rt_point_light(C.Structure):
     _fields_ = [("position", C.c_double * 3), ("color", C.c_double * 3)]
+
+
+class rt_light(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("reserved", C.c_int32),
+        ("position", C.c_double * 3),
+        ("direction", C.c_double * 3),
+        ("color", C.c_double * 3),
+        ("cutoff", C.c_double),
+        ("exponent", C.c_double),
+    ]
 
 
 class rt_object(C.Structure):
@@ -67,6 +82,9 @@ class rt_scene(C.Structure):
         ("program_code_words", C.c_int32),
         ("program_const_count", C.c_int32),
         ("reserved0", C.c_int32),
+        ("ext_lights", C.POINTER(rt_light)),
+        ("num_ext_lights", C.c_int32),
+        ("reserved1", C.c_int32),
     ]
 
 
@@ -100,9 +118,10 @@ class rt_stats(C.Structure):
 class PackedScene:
     """Owns the ctypes arrays an rt_scene points into (keeps them alive)."""
 
-    def __init__(self, scene, lights, objects, materials, programs=None):
+    def __init__(self, scene, lights, objects, materials, programs=None, ext_lights=None):
         self.scene = scene
         self._lights = lights
+        self._ext_lights = ext_lights
         self._objects = objects
         self._materials = materials
         # (code, consts, entry ctypes arrays, [(SurfaceFn, EvalState stack)] per program)
@@ -126,7 +145,8 @@ class PackedScene:
 # plane : 33 + 5 (denom) + 7 (numerator) ... = 45 on the non-parallel path
 # cube  : 6 planes = 270 (the reference re-transforms the ray per face)
 # cylinder: 33 + ~51 = 84
-FLOPS_PER_TEST = (52, 45, 270, 84)
+# cone (extension): 33 + a, halfB, c (15) + discriminant (3) + base cap (~10) = 61
+FLOPS_PER_TEST = (52, 45, 270, 84, 61)
 # Per shaded hit: surface props + ambient (21); per light: lighting (68).
 FLOPS_PER_SHADE = 21
 FLOPS_PER_LIGHT = 68

@@ -16,7 +16,7 @@ import os
 import sys
 
 
-def render_program(path, out_dir=None, device=0, stats=False, log=sys.stdout):
+def render_program(path, out_dir=None, device=0, stats=False, log=sys.stdout, extensions=False):
     from . import gml, imageio, scene
     from .render import RenderContext
     ctx = RenderContext(device)
@@ -39,7 +39,7 @@ def render_program(path, out_dir=None, device=0, stats=False, log=sys.stdout):
             print(json.dumps(d), file=log)
 
     try:
-        st = gml.EvalState(render=hook)
+        st = gml.EvalState(render=hook, extensions=extensions)
         st.parse_and_eval_file(path)
     finally:
         ctx.close()
@@ -52,11 +52,13 @@ def main(argv=None):
     ap.add_argument("--out-dir", default=None)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--extensions", action="store_true",
+                    help="enable cone, light, spotlight, real (ICFP operators the reference lacks)")
     a = ap.parse_args(argv)
     if a.out_dir:
         os.makedirs(a.out_dir, exist_ok=True)
     for f in a.files:
-        for w in render_program(f, a.out_dir, a.device, a.stats):
+        for w in render_program(f, a.out_dir, a.device, a.stats, extensions=a.extensions):
             print("wrote", w)
     return 0
 

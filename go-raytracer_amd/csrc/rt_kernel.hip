@@ -80,10 +80,12 @@ using namespace rt;
 // mats   [nmat][MAT]  0..2 colour, 3 reflectivity, 4..5 baked fuzz offset
 //                     (fuzz*cos^2, fuzz*sin^2; raytracer.go:517-521), 6 fuzz>=0,
 //                     7 transparency, 8 ior, 9 kd, 10 ks, 11 specular exponent
-// lights [nl][LGT]    0..2 position, 3..5 colour
+// lights [nl][LGT]    0..2 position, 3..5 colour, 6..8 directional: normalize(-dir),
+//                     spot: normalize(at - pos); 9 kind, 10 spot cos(cutoff),
+//                     11 spot exponent (kinds: include/rt_abi.h RT_LIGHT_*)
 // kind   [nobj] int32;  objmat [nobj][OMAT] int32 per-face material index
 // ---------------------------------------------------------------------------
-enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8, GLOB = 16 };
+enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
 // GLOB record (head of the lights section): 0..2 ambient, 3..5 bg start,
 // 6..8 bg end, 9 viewport width, 10 viewport height (read where used, so they
 // do not occupy scalar registers across the whole kernel)
@@ -94,7 +96,8 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 8, OMAT = 8, GLOB = 16 };
 // material is both reflective and transparent) always live in HBM.
 enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
-enum { ST_SHADOW = 0, ST_TRACED = 1, ST_STESTS = 2, ST_SHADED = 6, ST_SURFERR = 7, ST_COUNT = 8, ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24 };
+enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
+       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24 };
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
 #ifndef RT_LDS_MAX
 #define RT_LDS_MAX (40 * 1024)
@@ -127,7 +130,8 @@ struct Params {
 // Per-lane event counters (u64, LDS, fire-and-forget ds_add), reduced once per
 // workgroup at exit: per-wave 64-bit SGPR counters pushed the kernel into
 // SGPR spilling (C2 +33% time, C3 +7%).
-enum { CNT_TRACED = 0, CNT_SHADED = 1, CNT_SURFERR = 2, CNT_ST0 = 3, NCNT = 7 };
+enum { CNT_TRACED = 0, CNT_SHADED = 1, CNT_SURFERR = 2, CNT_ST0 = 3, NCNT = CNT_ST0 + RT_NUM_KINDS };
+enum { PREF = 8 };  // u32 per prefix-count entry (RT_NUM_KINDS used, 16-B aligned)
 // BVH node: child 0 box (lo xyz, hi xyz), child 1 box, then as int: ref 0,
 // ref 1, smallest object index under child 0, under child 1. A ref is
 // (node << 3) for an internal node, (first << 3) | count for a leaf of
@@ -255,13 +259,26 @@ __device__ __forceinline__ bool cube_hit(const Ray& l, double& t, int& face) {
 }
 
 // Cylinder.Intersect (raytracer.go:279-337).
-__device__ __forceinline__ bool cylinder_hit(const Ray& l, double& t, int& face) {
+// Cylinder.Intersect (raytracer.go:279-337) and, with cone = true, the
+// contest-extension cone (oracle/rt_oracle.c cone_intersect; not in the
+// reference): the same quadric-plus-caps structure, so one routine (the flag
+// is wave-uniform) keeps register pressure at the cylinder's. Every quantity
+// is formed in the oracle's op order: the cone's a, halfB, c0 append
+// "- dy*dy", "- oy*dy", "- oy*oy" where the cylinder has nothing / "- 1.0".
+__device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, bool cone) {
   double bestT = __builtin_inf();
   int bestFace = -1;
   double a = l.d.x * l.d.x + l.d.z * l.d.z;
-  if (a > 1e-12) {
-    double hb = l.o.x * l.d.x + l.o.z * l.d.z;
-    double c0 = l.o.x * l.o.x + l.o.z * l.o.z - 1.0;
+  double hb = l.o.x * l.d.x + l.o.z * l.d.z;
+  double c0 = l.o.x * l.o.x + l.o.z * l.o.z;
+  if (cone) {
+    a = a - l.d.y * l.d.y;
+    hb = hb - l.o.y * l.d.y;
+    c0 = c0 - l.o.y * l.o.y;
+  } else {
+    c0 = c0 - 1.0;
+  }
+  if (__builtin_fabs(a) > 1e-12) {  // cylinder: a >= 0, the reference's a > 1e-12
     double disc = hb * hb - a * c0;
     if (disc >= 0.0) {
       double sq = __builtin_sqrt(disc);
@@ -285,6 +302,16 @@ __device__ __forceinline__ bool cylinder_hit(const Ray& l, double& t, int& face)
         }
       }
     }
+  } else if (cone && __builtin_fabs(hb) > 1e-12) {  // cone: ray parallel to a generator
+    double n0 = -c0, den = 2.0 * hb;
+    if (!t_nonpos(n0, den)) {
+      double t0 = n0 / den;
+      double y0 = l.o.y + l.d.y * t0;
+      if (y0 >= 0.0 && y0 <= 1.0 && t0 > 0.0 && t0 < bestT) {
+        bestT = t0;
+        bestFace = 0;
+      }
+    }
   }
   if (__builtin_fabs(l.d.y) > 1e-12) {
     double nTop = 1.0 - l.o.y;
@@ -297,7 +324,7 @@ __device__ __forceinline__ bool cylinder_hit(const Ray& l, double& t, int& face)
       }
     }
     double nBot = -l.o.y;
-    if (!t_nonpos(nBot, l.d.y)) {
+    if (!cone && !t_nonpos(nBot, l.d.y)) {
       double tBot = nBot / l.d.y;
       double px = l.o.x + l.d.x * tBot, pz = l.o.z + l.d.z * tBot;
       if (px * px + pz * pz <= 1.0 && tBot > 0.0 && tBot < bestT) {
@@ -312,6 +339,7 @@ __device__ __forceinline__ bool cylinder_hit(const Ray& l, double& t, int& face)
   return true;
 }
 
+
 // One SceneObject.Intersect on a world-space ray; k is wave-uniform.
 __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r, double& t, int& face) {
   Ray l = to_obj(g, r);
@@ -323,8 +351,8 @@ __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r,
       return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
     case RT_CUBE:
       return cube_hit(l, t, face);
-    default:
-      return cylinder_hit(l, t, face);
+    default:  // RT_CYLINDER, RT_CONE
+      return quadric_hit(l, t, face, k == RT_CONE);
   }
 }
 
@@ -574,7 +602,7 @@ struct View {
   const double* lights;
   const int* kind;
   const int* objmat;
-  const uint32_t* pref;  // [nobj + 1][4]: objects of each kind with index < i
+  const uint32_t* pref;  // [nobj + 1][PREF]: objects of each kind with index < i
 };
 
 template <bool LDS, bool BVH>
@@ -955,8 +983,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               s[8] * p.x + s[9] * p.y + s[10] * p.z + s[11]);
       if (k == RT_SPHERE) {
         nw = p;
-      } else if (k == RT_CYLINDER) {
-        d3 n = hit_f == 0 ? mk(p.x, 0, p.z) : (hit_f == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
+      } else if (k == RT_CYLINDER || k == RT_CONE) {
+        d3 n = hit_f == 0 ? (k == RT_CONE ? mk(p.x, -p.y, p.z) : mk(p.x, 0, p.z))
+                          : (hit_f == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
         // NormalMat = WorldToObject^T (raytracer.go:814): MulDir then Normalize.
         nw = norm(mk(g[0] * n.x + g[4] * n.y + g[8] * n.z, g[1] * n.x + g[5] * n.y + g[9] * n.z,
                      g[2] * n.x + g[6] * n.y + g[10] * n.z));
@@ -974,7 +1003,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           bad = __builtin_fabs(p.y) > 1;
           v = (p.y + 1.0) / 2.0;
           u = go_acos(p.z / __builtin_sqrt(1.0 - p.y * p.y)) / 6.283185307179586;
-        } else if (k == RT_CYLINDER && hit_f == 0) {
+        } else if ((k == RT_CYLINDER || k == RT_CONE) && hit_f == 0) {
           u = (go_atan2(p.x, p.z) + 3.141592653589793) / 6.283185307179586;
           v = p.y;
         } else {
@@ -1015,12 +1044,20 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (hit) L = scale(mk(G[0], G[1], G[2]), M[9]);
     const double rlen = len(ray.d);
     const d3 sorig = add(pw, scale(nw, 1e-4));
-    uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind
+    uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind (cones: below)
     for (int li = 0; li < P.nlights; li++) {
       const double* lt = S.lights + (size_t)li * LGT;
-      d3 lth = sub(mk(lt[0], lt[1], lt[2]), pw);
-      double dist = len(lth);
-      d3 ldir = norm(lth);
+      const int lkind = (int)lt[9];  // wave-uniform
+      d3 ldir;
+      double dist;
+      if (lkind == RT_LIGHT_DIRECTIONAL) {  // extension: light at infinity
+        ldir = mk(lt[6], lt[7], lt[8]);
+        dist = __builtin_inf();
+      } else {
+        d3 lth = sub(mk(lt[0], lt[1], lt[2]), pw);
+        dist = len(lth);
+        ldir = norm(lth);
+      }
       bool open = hit;  // lanes still looking for an occluder
       Ray sr;
       sr.o = sorig;
@@ -1127,16 +1164,22 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         send = open ? P.nobj : occ + 1;
       }
       if (hit) {
-        const uint4 pe = *reinterpret_cast<const uint4*>(S.pref + (size_t)send * 4);
+        const uint4 pe = *reinterpret_cast<const uint4*>(S.pref + (size_t)send * PREF);
+        const uint32_t pe4 = S.pref[(size_t)send * PREF + 4];
         const int hk = hit_i < send ? S.kind[hit_i] : -1;
         sc0 += pe.x - (hk == 0 ? 1u : 0u);
         sc1 += pe.y - (hk == 1 ? 1u : 0u);
         sc2 += pe.z - (hk == 2 ? 1u : 0u);
         sc3 += pe.w - (hk == 3 ? 1u : 0u);
+        if (P.kind_mask & 16) cnt_add(CNT_ST0 + 4, pe4 - (hk == 4 ? 1u : 0u));  // cones: rare, flushed per light
       }
       PH_MARK(4);
       if (hit && open) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
+        if (lkind == RT_LIGHT_SPOT) {  // extension: cone falloff
+          const double ca = dot(neg(ldir), mk(lt[6], lt[7], lt[8]));
+          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11]) : 0.0);
+        }
         double ndl = go_max(0, dot(nw, ldir));
         d3 diffuse = scale(lcol, ndl * M[9]);
         d3 H = norm(add(neg(ray.d), ldir));
@@ -1706,7 +1749,9 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     s.bg1[k] = in->bg_end[k];
   }
   s.nobj = in->num_objects;
-  s.nlights = in->num_lights;
+  const bool ext_lights = in->num_ext_lights > 0;
+  if (ext_lights && !in->ext_lights) return fail(RT_E_INVALID, "ext_lights is NULL");
+  s.nlights = ext_lights ? in->num_ext_lights : in->num_lights;
   s.nmats = in->num_materials;
 
   std::vector<double> geo((size_t)s.nobj * GEO, 0.0), shade((size_t)s.nobj * SHD, 0.0);
@@ -1737,8 +1782,8 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       // World-space bounding sphere of the unit primitive: centre = O2W(local
       // centre), radius <= ||L||_F * local radius (spectral <= Frobenius),
       // padded for FP32 culling (see may_hit). Stored as 4 floats in 12..13.
-      const double lc[4][3] = {{0, 0, 0}, {0, 0, 0}, {0.5, 0.5, 0.5}, {0, 0.5, 0}};
-      const double lr[4] = {1.0, 0.0, 0.8660254037844387, 1.118033988749895};
+      const double lc[RT_NUM_KINDS][3] = {{0, 0, 0}, {0, 0, 0}, {0.5, 0.5, 0.5}, {0, 0.5, 0}, {0, 0.5, 0}};
+      const double lr[RT_NUM_KINDS] = {1.0, 0.0, 0.8660254037844387, 1.118033988749895, 1.118033988749895};
       double fro = 0.0;
       for (int r = 0; r < 3; r++)
         for (int k = 0; k < 3; k++) fro += o2w.m[r][k] * o2w.m[r][k];
@@ -1824,11 +1869,39 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   }
   lights[9] = s.vw;
   lights[10] = s.vh;
-  for (int l = 0; l < s.nlights; l++)
-    for (int k = 0; k < 3; k++) {
-      lights[GLOB + (size_t)l * LGT + k] = in->lights[l].position[k];
-      lights[GLOB + (size_t)l * LGT + 3 + k] = in->lights[l].color[k];
+  for (int l = 0; l < s.nlights; l++) {
+    double* L = &lights[GLOB + (size_t)l * LGT];
+    if (!ext_lights) {
+      for (int k = 0; k < 3; k++) {
+        L[k] = in->lights[l].position[k];
+        L[3 + k] = in->lights[l].color[k];
+      }
+      continue;
     }
+    // contest-extension lights (oracle/rt_oracle.c convert_scene)
+    const rt_light& e = in->ext_lights[l];
+    if (e.kind < RT_LIGHT_POINT || e.kind > RT_LIGHT_SPOT) return fail(RT_E_INVALID, "unknown light kind");
+    for (int k = 0; k < 3; k++) {
+      L[k] = e.position[k];
+      L[3 + k] = e.color[k];
+    }
+    L[9] = (double)e.kind;
+    double d[3] = {e.direction[0], e.direction[1], e.direction[2]};
+    if (e.kind == RT_LIGHT_DIRECTIONAL)
+      for (int k = 0; k < 3; k++) d[k] = -d[k];
+    if (e.kind == RT_LIGHT_SPOT)
+      for (int k = 0; k < 3; k++) d[k] = d[k] - e.position[k];
+    if (e.kind != RT_LIGHT_POINT) {  // vec.go:78 Normalize
+      const double m = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+      for (int k = 0; k < 3; k++) L[6 + k] = d[k] / m;
+    }
+    if (e.kind == RT_LIGHT_SPOT) {
+      double cc;
+      if (!go_cos(e.cutoff * 0.017453292519943295, cc)) return fail(RT_E_INVALID, "spot cutoff outside restated range");
+      L[10] = cc;
+      L[11] = e.exponent;
+    }
+  }
   // One blob: geo | shade | mats | lights | kind | objmat (16-B aligned sections).
   s.off_geo = 0;
   s.off_shade = align16(s.off_geo + (int)(geo.size() * sizeof(double)));
@@ -1870,10 +1943,10 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   }
   s.num_programs = nprog;
   // per-kind prefix counts (shadow-test counters)
-  std::vector<uint32_t> prefb((size_t)(s.nobj + 1) * 4, 0u);
+  std::vector<uint32_t> prefb((size_t)(s.nobj + 1) * PREF, 0u);
   for (int i = 0; i < s.nobj; i++) {
-    for (int k = 0; k < 4; k++) prefb[(size_t)(i + 1) * 4 + k] = prefb[(size_t)i * 4 + k];
-    prefb[(size_t)(i + 1) * 4 + kind[i]]++;
+    for (int k = 0; k < RT_NUM_KINDS; k++) prefb[(size_t)(i + 1) * PREF + k] = prefb[(size_t)i * PREF + k];
+    prefb[(size_t)(i + 1) * PREF + kind[i]]++;
   }
   s.off_prefb = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
   s.off_code = align16(s.off_prefb + (int)(prefb.size() * sizeof(uint32_t)));
@@ -2087,13 +2160,13 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
   HIP_TRY(hipStreamSynchronize(st));
   std::memset(out, 0, sizeof *out);
   // Intersect calls from closestHit: every traced ray tests every object.
-  uint64_t per_kind[4] = {0, 0, 0, 0};
+  uint64_t per_kind[RT_NUM_KINDS] = {0, 0, 0, 0, 0};
   if (c->has_scene)
     for (int k : c->sc.kinds) per_kind[k]++;
   out->primary_rays = c->primary_pending;
   out->secondary_rays = h[ST_TRACED] - c->primary_pending;
   out->shadow_rays = h[ST_SHADOW];
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < RT_NUM_KINDS; k++) {
     out->tests[k] = h[ST_TRACED] * per_kind[k];
     out->shadow_tests[k] = h[ST_STESTS + k];
   }

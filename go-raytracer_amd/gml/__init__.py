@@ -16,17 +16,18 @@ def _hook(out):
     return render
 
 
-def run_file(path):
+def run_file(path, extensions=False):
     """Evaluate a .gml file; returns the list of (RenderArgs, EvalState) it
-    rendered (in order) and the final EvalState."""
+    rendered (in order) and the final EvalState. extensions=True enables the
+    ICFP operators the reference lacks (cone, light, spotlight, real)."""
     out = []
-    st = EvalState(render=_hook(out))
+    st = EvalState(render=_hook(out), extensions=extensions)
     st.parse_and_eval_file(path)
     return out, st
 
 
-def run_text(text):
+def run_text(text, extensions=False):
     out = []
-    st = EvalState(render=_hook(out))
+    st = EvalState(render=_hook(out), extensions=extensions)
     st.parse_and_eval(text)
     return out, st

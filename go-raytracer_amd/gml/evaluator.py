@@ -141,12 +141,16 @@ def debug_str(v, idmap):
 class EvalState:
     """EvalState (evaluator.go:43-50)."""
 
-    def __init__(self, render=None):
+    def __init__(self, render=None, extensions=False):
         self.stack = []
         self.ids = X.IDMapping()
         self.env = {}
         self.render = render
         self.cur = None
+        # ICFP 2000 operators the reference lacks (cone, light, spotlight,
+        # real): off by default, so programs behave exactly as in the reference
+        # ("unbound identifier" for these names).
+        self.extensions = extensions
 
     # -- program entry points (evaluator.go:305-356) --
     def parse_and_eval(self, text):
@@ -156,7 +160,7 @@ class EvalState:
         self.eval(X.parse_file(path, self.ids))
 
     def clone(self):
-        c = EvalState(self.render)
+        c = EvalState(self.render, self.extensions)
         c.stack = list(self.stack)
         c.ids = self.ids.clone()
         c.env = dict(self.env)
@@ -185,6 +189,8 @@ class EvalState:
             self.env[tok.id] = self.pop()
         elif t is X.Identifier:
             b = BUILTINS.get(tok.name)
+            if b is None and self.extensions:
+                b = EXT_BUILTINS.get(tok.name)
             if b is not None:
                 b(self)
                 return
@@ -249,7 +255,7 @@ def _closure(e):
     return e.pop_t(VClosure, "gml.VClosure")
 
 
-_SCENE_TYPES = (S.Sphere, S.Cube, S.Cylinder, S.Plane, S.Union, S.Difference)
+_SCENE_TYPES = (S.Sphere, S.Cube, S.Cylinder, S.Plane, S.Union, S.Difference, S.Cone)
 
 
 def _sceneobj(e):
@@ -494,8 +500,9 @@ def pop_render_args(e):
     lights = e.pop_t(VArray, "gml.VArray")
     amb = _vec(e)
     ls = []
+    ok = (S.PointLight, S.DirectionalLight, S.SpotLight) if e.extensions else (S.PointLight,)
     for l in lights.elements:
-        if not isinstance(l, S.PointLight):
+        if not isinstance(l, ok):
             raise GMLError("expected lights array to contain *PointLight, got %s" % type(l).__name__)
         ls.append(l)
     return S.RenderArgs(ambient=tuple(amb), lights=ls, scene=obj, depth=int(depth), fov=float(fov),
@@ -589,3 +596,34 @@ def b_floor2(e):
 
 
 BUILTINS["floor"] = b_floor2
+
+
+# ---- contest extensions (ICFP 2000 task; not in the reference, parity-unpinned) ----
+
+def b_cone(e):
+    e.stack.append(S.Cone(_surface(e)))
+
+
+def b_light(e):
+    """`dir color light`: directional light travelling along dir."""
+    color = _vec(e)
+    d = _vec(e)
+    e.stack.append(S.DirectionalLight(tuple(d), tuple(color)))
+
+
+def b_spotlight(e):
+    """`pos at color cutoff exp spotlight`."""
+    exp = float(_real(e))
+    cutoff = float(_real(e))
+    color = _vec(e)
+    at = _vec(e)
+    pos = _vec(e)
+    e.stack.append(S.SpotLight(tuple(pos), tuple(at), tuple(color), cutoff, exp))
+
+
+def b_real(e):
+    """`i real`: Go float64(int64) (round to nearest)."""
+    e.stack.append(VReal(float(int(_int(e)))))
+
+
+EXT_BUILTINS = {"cone": b_cone, "light": b_light, "spotlight": b_spotlight, "real": b_real}

@@ -28,6 +28,8 @@ def render_args_lines(args, idmap):
         ind[0] -= 1
     add("ambient: " + f3(args.ambient))
     for l in args.lights:
+        if not isinstance(l, S.PointLight):
+            raise TypeError("unknown light type %s" % type(l).__name__)
         add("light:")
         ind[0] += 1
         add("position: " + f3(l.position))

@@ -57,7 +57,7 @@ def load_library(path=None):
     l.rt_ssim_rgba8.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
     l.rt_render.restype = i
-    if l.rt_abi_version() != 1:
+    if l.rt_abi_version() != abi.RT_ABI_VERSION:
         raise RenderError("librtamd ABI version mismatch")
     _lib = l
     return l

@@ -50,6 +50,25 @@ class PointLight:
     color: tuple
 
 
+@dataclass(frozen=True)
+class DirectionalLight:
+    """Contest extension (GML `light`, not in the reference): light at infinity
+    travelling along `direction` (include/rt_abi.h rt_light)."""
+    direction: tuple
+    color: tuple
+
+
+@dataclass(frozen=True)
+class SpotLight:
+    """Contest extension (GML `spotlight`, not in the reference): at `position`,
+    aimed at point `at`, cutoff half-angle in degrees, falloff exponent."""
+    position: tuple
+    at: tuple
+    color: tuple
+    cutoff: float
+    exponent: float
+
+
 class SceneObject:
     """gml.SceneObject (evaluator.go:152-156): Transform composes existing.MulMat(new)."""
 
@@ -100,6 +119,14 @@ class Cube(SceneObject):
 class Cylinder(SceneObject):
     """Unit cylinder x^2+z^2<=1, 0<=y<=1 (evaluator.go:206-223). Per-face surface:
     (side, top, bottom) (raytracer.go:263-267)."""
+    surface: object = Material()
+    transform_mat: Optional[list] = None
+
+
+@dataclass(frozen=True)
+class Cone(SceneObject):
+    """Contest extension (GML `cone`, not in the reference renderer): apex at the
+    origin, x^2 + z^2 = y^2 for 0 <= y <= 1, base at y = 1. Faces (side, base)."""
     surface: object = Material()
     transform_mat: Optional[list] = None
 
@@ -157,8 +184,9 @@ class RenderArgs:
     state: object = None
 
 
-_NFACES = {abi.RT_SPHERE: 1, abi.RT_PLANE: 1, abi.RT_CUBE: 6, abi.RT_CYLINDER: 3}
-_KIND = {Sphere: abi.RT_SPHERE, Plane: abi.RT_PLANE, Cube: abi.RT_CUBE, Cylinder: abi.RT_CYLINDER}
+_NFACES = {abi.RT_SPHERE: 1, abi.RT_PLANE: 1, abi.RT_CUBE: 6, abi.RT_CYLINDER: 3, abi.RT_CONE: 2}
+_KIND = {Sphere: abi.RT_SPHERE, Plane: abi.RT_PLANE, Cube: abi.RT_CUBE, Cylinder: abi.RT_CYLINDER,
+         Cone: abi.RT_CONE}
 
 
 def flatten(root):
@@ -250,16 +278,45 @@ def convert(args: RenderArgs) -> abi.PackedScene:
         cm.kd = m.kd
         cm.ks = m.ks
         cm.specular_exponent = m.specular_exponent
+    ext = any(not isinstance(l, PointLight) for l in args.lights)
     c_lights = (abi.rt_point_light * max(1, len(args.lights)))()
-    for i, l in enumerate(args.lights):
-        for k in range(3):
-            c_lights[i].position[k] = float(l.position[k])
-            c_lights[i].color[k] = float(l.color[k])
+    c_ext = None
+    if not ext:
+        for i, l in enumerate(args.lights):
+            for k in range(3):
+                c_lights[i].position[k] = float(l.position[k])
+                c_lights[i].color[k] = float(l.color[k])
+    else:  # contest-extension lights: the whole list, in program order
+        c_ext = (abi.rt_light * len(args.lights))()
+        for i, l in enumerate(args.lights):
+            e = c_ext[i]
+            for k in range(3):
+                e.color[k] = float(l.color[k])
+            if isinstance(l, PointLight):
+                e.kind = abi.RT_LIGHT_POINT
+                for k in range(3):
+                    e.position[k] = float(l.position[k])
+            elif isinstance(l, DirectionalLight):
+                e.kind = abi.RT_LIGHT_DIRECTIONAL
+                for k in range(3):
+                    e.direction[k] = float(l.direction[k])
+            elif isinstance(l, SpotLight):
+                e.kind = abi.RT_LIGHT_SPOT
+                for k in range(3):
+                    e.position[k] = float(l.position[k])
+                    e.direction[k] = float(l.at[k])
+                e.cutoff = float(l.cutoff)
+                e.exponent = float(l.exponent)
+            else:
+                raise TypeError("unknown light type %s" % type(l).__name__)
     sc = abi.rt_scene()
     sc.width = int(args.width)
     sc.height = int(args.height)
     sc.depth = int(args.depth)
-    sc.num_lights = len(args.lights)
+    sc.num_lights = 0 if ext else len(args.lights)
+    if ext:
+        sc.ext_lights = C.cast(c_ext, C.POINTER(abi.rt_light))
+        sc.num_ext_lights = len(args.lights)
     sc.fov = float(args.fov)
     for k in range(3):
         sc.ambient[k] = float(args.ambient[k])
@@ -293,4 +350,4 @@ def convert(args: RenderArgs) -> abi.PackedScene:
         sc.program_code_words = len(words)
         sc.program_const_count = len(consts)
         packed_progs = (c_code, c_consts, c_entry, [sf for sf, _ in programs], args.state)
-    return abi.PackedScene(sc, c_lights, c_objs, c_mats, packed_progs)
+    return abi.PackedScene(sc, c_lights, c_objs, c_mats, packed_progs, c_ext)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* Status codes. */
 #define RT_OK 0
@@ -48,7 +48,11 @@ extern "C" {
 #define RT_PLANE 1
 #define RT_CUBE 2
 #define RT_CYLINDER 3
-#define RT_NUM_KINDS 4
+/* Contest extension (ICFP 2000 GML `cone`; not in the reference renderer, so
+ * parity-unpinned): apex at the origin, x^2 + z^2 = y^2 for 0 <= y <= 1,
+ * base disk at y = 1. Faces 0 side, 1 base. */
+#define RT_CONE 4
+#define RT_NUM_KINDS 5
 
 #define RT_MAX_FACES 6 /* prim.NUM_CUBE_SIDES, internal/prim/plane.go:27 */
 
@@ -69,6 +73,27 @@ typedef struct rt_point_light {
     double position[3];
     double color[3];
 } rt_point_light;
+
+/* Lights of the contest extensions (GML `light`, `spotlight`; not in the
+ * reference renderer, parity-unpinned). Point lights here behave exactly like
+ * rt_point_light. Directional: direction = the way the light travels; the
+ * shading vector is normalize(-direction) and shadow rays are unbounded.
+ * Spot: at position, aimed at `direction` (a point), cutoff half-angle in
+ * degrees, intensity colour * Pow(cos(angle), exponent) inside the cone and 0
+ * outside (shadow rays are traced either way, one per light). No distance
+ * attenuation, matching the reference's point lights. */
+#define RT_LIGHT_POINT 0
+#define RT_LIGHT_DIRECTIONAL 1
+#define RT_LIGHT_SPOT 2
+typedef struct rt_light {
+    int32_t kind;
+    int32_t reserved;
+    double position[3];
+    double direction[3]; /* directional: direction; spot: the point aimed at */
+    double color[3];
+    double cutoff;       /* spot: degrees */
+    double exponent;     /* spot */
+} rt_light;
 
 /* One flattened scene object (a leaf of gml.RenderArgs.Scene after the BFS
  * union flattening of raytracer.go:776-828).
@@ -126,6 +151,11 @@ typedef struct rt_scene {
     int32_t program_code_words;
     int32_t program_const_count;
     int32_t reserved0;
+    /* ABI 2: when num_ext_lights > 0 these are the scene's lights, in program
+     * order, and lights / num_lights are ignored. */
+    const rt_light *ext_lights;
+    int32_t num_ext_lights;
+    int32_t reserved1;
 } rt_scene;
 
 /* Work counters, identical in the CPU oracle and the GPU path.

@@ -112,6 +112,12 @@ typedef struct {
     vec3 ambient, bg0, bg1;
     int nlights;
     vec3 *lpos, *lcol;
+    /* contest-extension lights (rt_light): kind, shading direction
+     * (directional: normalize(-direction)) or spot axis normalize(at - pos),
+     * cos(cutoff), exponent */
+    int *lkind;
+    vec3 *ldir;
+    double *lcos, *lexp;
     int nobj;
     object *obj;
     const rt_material *mats;
@@ -223,6 +229,46 @@ static int cylinder_intersect(const object *o, ray r, double *t, vec3 *p, int *f
     return 1;
 }
 
+/* Contest extension (not in the reference; parity-unpinned): unit cone,
+ * x^2 + z^2 = y^2 for 0 <= y <= 1 (face 0), base disk at y = 1 (face 1);
+ * smallest t > 0 over both roots of the side and the base, in that order,
+ * written in the style of the reference's cylinder. A ray parallel to a
+ * generator (a == 0) has the single root -c / (2 halfB). */
+static int cone_intersect(const object *o, ray r, double *t, vec3 *p, int *face) {
+    r = to_object(r, &o->w2o);
+    double bestT = INFINITY;
+    int bestFace = -1;
+    vec3 bestP = V(0, 0, 0);
+#define CONSIDER(tt, ff, pp) do { if ((tt) > 0.0 && (tt) < bestT) { bestT = (tt); bestFace = (ff); bestP = (pp); } } while (0)
+    double a = r.dir.x * r.dir.x + r.dir.z * r.dir.z - r.dir.y * r.dir.y;
+    double halfB = r.origin.x * r.dir.x + r.origin.z * r.dir.z - r.origin.y * r.dir.y;
+    double c0 = r.origin.x * r.origin.x + r.origin.z * r.origin.z - r.origin.y * r.origin.y;
+    if (fabs(a) > 1e-12) {
+        double disc = halfB * halfB - a * c0;
+        if (disc >= 0.0) {
+            double sq = sqrt(disc);
+            double ts[2] = {(-halfB - sq) / a, (-halfB + sq) / a};
+            for (int k = 0; k < 2; k++) {
+                vec3 pt = v_add(r.origin, v_scale(r.dir, ts[k]));
+                if (pt.y >= 0.0 && pt.y <= 1.0) CONSIDER(ts[k], 0, pt);
+            }
+        }
+    } else if (fabs(halfB) > 1e-12) {
+        double t0 = -c0 / (2.0 * halfB);
+        vec3 pt = v_add(r.origin, v_scale(r.dir, t0));
+        if (pt.y >= 0.0 && pt.y <= 1.0) CONSIDER(t0, 0, pt);
+    }
+    if (fabs(r.dir.y) > 1e-12) {
+        double tTop = (1.0 - r.origin.y) / r.dir.y;
+        vec3 pTop = v_add(r.origin, v_scale(r.dir, tTop));
+        if (pTop.x * pTop.x + pTop.z * pTop.z <= 1.0) CONSIDER(tTop, 1, pTop);
+    }
+#undef CONSIDER
+    if (bestFace == -1) return 0;
+    *t = bestT; *p = bestP; *face = bestFace;
+    return 1;
+}
+
 static int object_intersect(const object *o, ray r, double *t, vec3 *p, int *face) {
     *face = 0;
     switch (o->kind) {
@@ -230,12 +276,13 @@ static int object_intersect(const object *o, ray r, double *t, vec3 *p, int *fac
     case RT_PLANE: { ray lr = to_object(r, &o->w2o); return plane_intersect_obj(&o->face[0], lr, t, p); }
     case RT_CUBE: return cube_intersect(o, r, t, p, face);
     case RT_CYLINDER: return cylinder_intersect(o, r, t, p, face);
+    case RT_CONE: return cone_intersect(o, r, t, p, face);
     }
     return 0;
 }
 
 /* ---- per-thread counters ------------------------------------------------ */
-typedef struct { uint64_t secondary, shadow, tests[4], shadow_tests[4], shaded, surface_errors; } counters;
+typedef struct { uint64_t secondary, shadow, tests[RT_NUM_KINDS], shadow_tests[RT_NUM_KINDS], shaded, surface_errors; } counters;
 
 /* Closure surfaces: faces with a negative material index are evaluated by a
  * host callback that runs the GML interpreter (EvalSurfaceFn,
@@ -303,6 +350,12 @@ static void surface_props(const scene *s, const hit *h, hitex *x, counters *cnt)
         x->nw = v_norm(m_muldir(&o->normal_mat, n));
         break;
     }
+    case RT_CONE: {  /* extension: gradient of x^2 + z^2 - y^2, NormalMat as the cylinder */
+        vec3 n = h->face == 0 ? V(h->p.x, -h->p.y, h->p.z) : V(0, 1, 0);
+        x->pw = m_mulpoint(&o->o2w, h->p);
+        x->nw = v_norm(m_muldir(&o->normal_mat, n));
+        break;
+    }
     }
     int mi = o->material[h->face];
     if (mi >= 0) {
@@ -323,6 +376,7 @@ static void surface_props(const scene *s, const hit *h, hitex *x, counters *cnt)
         v = h->p.z;
         break;
     case RT_CYLINDER:                                                           /* :339-359 */
+    case RT_CONE:  /* extension: the cylinder's coordinates */
         if (h->face == 0) {
             u = (go_atan2(h->p.x, h->p.z) + M_PI) / (2.0 * M_PI);
             v = h->p.y;
@@ -356,16 +410,27 @@ static vec3 compute_lighting(const scene *s, const hit *h, const hitex *x, ray r
     const rt_material *mat = x->mat;
     vec3 result = v_scale(s->ambient, mat->kd);
     for (int li = 0; li < s->nlights; li++) {
-        vec3 lth = v_sub(s->lpos[li], x->pw);
-        double dist = v_len(lth);
-        vec3 ldir = v_norm(lth);
+        vec3 lth, ldir, lcol = s->lcol[li];
+        double dist;
+        if (s->lkind[li] == RT_LIGHT_DIRECTIONAL) {  /* extension: light at infinity */
+            ldir = s->ldir[li];
+            dist = INFINITY;
+        } else {
+            lth = v_sub(s->lpos[li], x->pw);
+            dist = v_len(lth);
+            ldir = v_norm(lth);
+        }
+        if (s->lkind[li] == RT_LIGHT_SPOT) {          /* extension: cone falloff */
+            double ca = v_dot(v_neg(ldir), s->ldir[li]);
+            lcol = v_scale(lcol, ca >= s->lcos[li] ? go_pow(ca, s->lexp[li]) : 0.0);
+        }
         cnt->shadow++;
         if (in_shadow(s, h, x, ldir, dist, r, cnt)) continue;
         double ndl = go_max(0, v_dot(x->nw, ldir));
-        vec3 diffuse = v_scale(s->lcol[li], ndl * mat->kd);
+        vec3 diffuse = v_scale(lcol, ndl * mat->kd);
         vec3 H = v_norm(v_add(Vv, ldir));
         double spec = go_max(0, v_dot(x->nw, H));
-        vec3 specular = v_scale(s->lcol[li], mat->ks * go_pow(spec, mat->specular_exponent));
+        vec3 specular = v_scale(lcol, mat->ks * go_pow(spec, mat->specular_exponent));
         result = v_add(v_add(result, diffuse), specular);
     }
     return result;
@@ -457,12 +522,33 @@ static int convert_scene(const rt_scene *in, scene *s) {
     s->ambient = V(in->ambient[0], in->ambient[1], in->ambient[2]);
     s->bg0 = V(in->bg_start[0], in->bg_start[1], in->bg_start[2]);
     s->bg1 = V(in->bg_end[0], in->bg_end[1], in->bg_end[2]);
-    s->nlights = in->num_lights;
-    s->lpos = (vec3 *)calloc((size_t)(in->num_lights + 1), sizeof(vec3));
-    s->lcol = (vec3 *)calloc((size_t)(in->num_lights + 1), sizeof(vec3));
-    for (int i = 0; i < in->num_lights; i++) {
-        s->lpos[i] = V(in->lights[i].position[0], in->lights[i].position[1], in->lights[i].position[2]);
-        s->lcol[i] = V(in->lights[i].color[0], in->lights[i].color[1], in->lights[i].color[2]);
+    const int ext = in->num_ext_lights > 0;
+    if (ext && !in->ext_lights) return RT_E_INVALID;
+    s->nlights = ext ? in->num_ext_lights : in->num_lights;
+    s->lpos = (vec3 *)calloc((size_t)(s->nlights + 1), sizeof(vec3));
+    s->lcol = (vec3 *)calloc((size_t)(s->nlights + 1), sizeof(vec3));
+    s->ldir = (vec3 *)calloc((size_t)(s->nlights + 1), sizeof(vec3));
+    s->lkind = (int *)calloc((size_t)(s->nlights + 1), sizeof(int));
+    s->lcos = (double *)calloc((size_t)(s->nlights + 1), sizeof(double));
+    s->lexp = (double *)calloc((size_t)(s->nlights + 1), sizeof(double));
+    for (int i = 0; i < s->nlights; i++) {
+        if (!ext) {
+            s->lpos[i] = V(in->lights[i].position[0], in->lights[i].position[1], in->lights[i].position[2]);
+            s->lcol[i] = V(in->lights[i].color[0], in->lights[i].color[1], in->lights[i].color[2]);
+            continue;
+        }
+        const rt_light *l = &in->ext_lights[i];
+        if (l->kind < RT_LIGHT_POINT || l->kind > RT_LIGHT_SPOT) return RT_E_INVALID;
+        s->lkind[i] = l->kind;
+        s->lpos[i] = V(l->position[0], l->position[1], l->position[2]);
+        s->lcol[i] = V(l->color[0], l->color[1], l->color[2]);
+        vec3 d = V(l->direction[0], l->direction[1], l->direction[2]);
+        if (l->kind == RT_LIGHT_DIRECTIONAL) s->ldir[i] = v_norm(v_neg(d));
+        if (l->kind == RT_LIGHT_SPOT) {
+            s->ldir[i] = v_norm(v_sub(d, s->lpos[i]));
+            s->lcos[i] = go_cos(l->cutoff * 0.017453292519943295);
+            s->lexp[i] = l->exponent;
+        }
     }
     s->mats = in->materials;
     s->nmats = in->num_materials;
@@ -500,7 +586,7 @@ static int convert_scene(const rt_scene *in, scene *s) {
 }
 
 static void free_scene(scene *s) {
-    free(s->lpos); free(s->lcol); free(s->obj);
+    free(s->lpos); free(s->lcol); free(s->ldir); free(s->lkind); free(s->lcos); free(s->lexp); free(s->obj);
 }
 
 /* ---- Render (raytracer.go:589-682) --------------------------------------- */
@@ -560,7 +646,7 @@ static void *worker(void *arg) {
     j->sum.shadow += cnt.shadow;
     j->sum.shaded += cnt.shaded;
     j->sum.surface_errors += cnt.surface_errors;
-    for (int k = 0; k < 4; k++) { j->sum.tests[k] += cnt.tests[k]; j->sum.shadow_tests[k] += cnt.shadow_tests[k]; }
+    for (int k = 0; k < RT_NUM_KINDS; k++) { j->sum.tests[k] += cnt.tests[k]; j->sum.shadow_tests[k] += cnt.shadow_tests[k]; }
     pthread_mutex_unlock(&j->lock);
     return NULL;
 }
@@ -598,7 +684,7 @@ int oracle_render_rows(const rt_scene *in, int y0, int y1, int threads, uint8_t 
         st->shadow_rays = j.sum.shadow;
         st->shaded_hits = j.sum.shaded;
         st->surface_errors = j.sum.surface_errors;
-        for (int k = 0; k < 4; k++) { st->tests[k] = j.sum.tests[k]; st->shadow_tests[k] = j.sum.shadow_tests[k]; }
+        for (int k = 0; k < RT_NUM_KINDS; k++) { st->tests[k] = j.sum.tests[k]; st->shadow_tests[k] = j.sum.shadow_tests[k]; }
     }
     free_scene(&s);
     return RT_OK;
@@ -633,6 +719,7 @@ int oracle_surface_normal(const rt_scene *in, int idx, int face, const double po
     if (rc != RT_OK || idx < 0 || idx >= s.nobj) { free_scene(&s); return rc != RT_OK ? rc : RT_E_INVALID; }
     if (s.obj[idx].kind == RT_CYLINDER && (face < 0 || face > 2)) { free_scene(&s); return RT_E_INVALID; } /* :355-356 */
     if (s.obj[idx].kind == RT_CUBE && (face < 0 || face >= 6)) { free_scene(&s); return RT_E_INVALID; }    /* :243-245 */
+    if (s.obj[idx].kind == RT_CONE && (face < 0 || face > 1)) { free_scene(&s); return RT_E_INVALID; }
     hit h = {idx, 0, V(point_obj[0], point_obj[1], point_obj[2]), face};
     hitex x;
     counters cnt;

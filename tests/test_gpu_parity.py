@@ -250,9 +250,10 @@ def test_shared_reciprocal_division_is_bit_exact():
     assert '"mismatches": 0' in r.stdout
 
 
-def _mixed_scene(seed, n, width, height, depth=5, dup=True):
+def _mixed_scene(seed, n, width, height, depth=5, dup=True, ext=False):
     """Random spheres/cubes/cylinders (rotated, non-uniformly scaled), two
-    planes (one tilted), duplicates that tie exactly in t, mixed materials."""
+    planes (one tilted), duplicates that tie exactly in t, mixed materials.
+    ext: also cones and directional / spot lights (contest extensions)."""
     import random
     rng = random.Random(seed)
     mats = [S.material((rng.random(), rng.random(), rng.random()), rng.choice([0.0, 0.0, 0.3, 0.7]),
@@ -260,7 +261,7 @@ def _mixed_scene(seed, n, width, height, depth=5, dup=True):
                        rng.random(), rng.random(), float(rng.choice([1, 5, 10, 50]))) for _ in range(6)]
     objs = []
     for i in range(n):
-        kind = rng.choice([S.Sphere, S.Cube, S.Cylinder])
+        kind = rng.choice([S.Sphere, S.Cube, S.Cylinder] + ([S.Cone, S.Cone] if ext else []))
         m = rng.choice(mats)
         o = kind(m) if kind is not S.Cube else kind(m)
         o = (o.scale(0.2 + rng.random() * 0.5, 0.2 + rng.random() * 0.5, 0.2 + rng.random() * 0.5)
@@ -274,6 +275,9 @@ def _mixed_scene(seed, n, width, height, depth=5, dup=True):
     rng.shuffle(objs)
     lights = [S.PointLight((5.0, 6.0, 0.0), (0.6, 0.6, 0.6)), S.PointLight((-4.0, 3.0, 2.0), (0.4, 0.5, 0.4)),
               S.PointLight((0.0, 8.0, 8.0), (0.3, 0.3, 0.3))]
+    if ext:
+        lights[1] = S.DirectionalLight((0.3, -1.0, 0.4), (0.4, 0.4, 0.5))
+        lights.append(S.SpotLight((0.0, 5.0, 4.0), (0.5, -1.0, 6.0), (0.7, 0.6, 0.5), 35.0, 3.0))
     return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=S.Union(tuple(objs)), depth=depth, fov=75.0,
                         width=width, height=height, bg_start=(0.0, 0.0, 0.0), bg_end=(0.5, 0.7, 1.0))
 
@@ -330,3 +334,40 @@ def test_cli_renders_gml_programs(tmp_path):
         img = rt.imageio.read_image(p)
         gold = np.asarray(Image.open(os.path.join(GOLDEN, "example_cylinder_%s.png" % CYL[os.path.basename(p)])).convert("RGB"))
         assert np.array_equal(img, gold)
+
+
+
+@pytest.mark.parametrize("seed,n", [(21, 6), (22, 30), (23, 150)])
+def test_extension_scenes_match_oracle(ctx, seed, n):
+    """Cones and directional / spot lights (contest extensions; semantics =
+    the oracle's restatement), linear and BVH flavours: exact bytes, counters."""
+    packed = rt.scene.convert(_mixed_scene(seed, n, 96, 64, ext=True))
+    assert packed.scene.num_ext_lights == 4
+    img, st = render(ctx, packed)
+    ref, ost = oracle_bind.render_rows(packed)
+    assert_same(img, ref, "ext seed %d n %d" % (seed, n))
+    assert st.as_dict() == ost.as_dict()
+    assert st.tests[rt.abi.RT_CONE] > 0
+
+
+def test_extension_gml_program_matches_oracle(ctx):
+    """A GML program using cone (closure-textured), light and spotlight."""
+    from go_raytracer_amd import gml
+    src = """
+    { /v /u /face u 8.0 mulf floor v 8.0 mulf floor addi 2 modi 0 eqi
+      { 0.9 0.2 0.2 point } { 0.9 0.9 0.9 point } if 0.8 0.3 4.0 } /checker
+    checker cone 0.0 -1.0 4.0 translate /c
+    { /v /u /face 0.5 0.6 0.7 point 1.0 0.1 2.0 } plane 0.0 -1.0 0.0 translate /p
+    0.2 0.2 0.2 point
+    [ 1.0 -1.0 0.5 point 0.6 0.6 0.6 point light
+      -2.0 4.0 1.0 point 0.0 -1.0 4.0 point 0.8 0.8 0.6 point 25.0 2.0 spotlight
+      3.0 3.0 0.0 point 0.3 0.3 0.3 point pointlight ]
+    c p union 3 60.0 128 96 "ext.ppm" render
+    """
+    rendered, _ = gml.run_text(src, extensions=True)
+    packed = rt.scene.convert(rendered[0][0])
+    assert packed.scene.num_programs >= 1
+    img, st = render(ctx, packed)
+    ref, ost = oracle_bind.render_rows(packed)
+    assert_same(img, ref, "extension program")
+    assert st.as_dict() == ost.as_dict() and st.surface_errors == 0
