@@ -371,3 +371,19 @@ def test_extension_gml_program_matches_oracle(ctx):
     ref, ost = oracle_bind.render_rows(packed)
     assert_same(img, ref, "extension program")
     assert st.as_dict() == ost.as_dict() and st.surface_errors == 0
+
+
+@pytest.mark.parametrize("name", ["checked-cube", "cube2", "fov", "rotate"])
+def test_fixture_gml_programs_match_oracle(ctx, name):
+    """Every render call of the reference's other renderable fixture programs
+    (internal/gml/testdata), at reduced size: HIP == oracle with counters."""
+    from go_raytracer_amd import gml
+    rendered, _ = gml.run_file(os.path.join(GML, name + ".gml"))
+    assert rendered
+    for args, _ in rendered:
+        args.width, args.height = min(args.width, 160), min(args.height, 100)
+        packed = rt.scene.convert(args)
+        img, st = render(ctx, packed)
+        ref, ost = oracle_bind.render_rows(packed)
+        assert_same(img, ref, "%s %s" % (name, args.file))
+        assert st.as_dict() == ost.as_dict()
