@@ -13,10 +13,12 @@ RT_E_SINGULAR = -2
 RT_E_DEVICE = -3
 RT_E_NOMEM = -4
 
-RT_SPHERE, RT_PLANE, RT_CUBE, RT_CYLINDER, RT_CONE = 0, 1, 2, 3, 4
-RT_NUM_KINDS = 5
+RT_SPHERE, RT_PLANE, RT_CUBE, RT_CYLINDER, RT_CONE, RT_CSG = 0, 1, 2, 3, 4, 5
+RT_NUM_KINDS = 6
 RT_MAX_FACES = 6
-KIND_NAMES = ("sphere", "plane", "cube", "cylinder", "cone")
+KIND_NAMES = ("sphere", "plane", "cube", "cylinder", "cone", "csg")
+RT_CSG_UNION, RT_CSG_INTERSECT, RT_CSG_DIFFERENCE = -1, -2, -3
+RT_CSG_MAX_LEAVES = 128
 RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_SPOT = 0, 1, 2
 
 
@@ -57,6 +59,10 @@ class rt_object(C.Structure):
         ("transform", C.c_double * 16),
         ("plane_point", C.c_double * 3),
         ("plane_normal", C.c_double * 3),
+        ("csg_first", C.c_int32),
+        ("csg_count", C.c_int32),
+        ("csg_code", C.c_int32),
+        ("csg_code_len", C.c_int32),
     ]
 
 
@@ -85,6 +91,10 @@ class rt_scene(C.Structure):
         ("ext_lights", C.POINTER(rt_light)),
         ("num_ext_lights", C.c_int32),
         ("reserved1", C.c_int32),
+        ("csg_leaves", C.POINTER(rt_object)),
+        ("csg_code", C.POINTER(C.c_int32)),
+        ("num_csg_leaves", C.c_int32),
+        ("csg_code_words", C.c_int32),
     ]
 
 
@@ -146,7 +156,9 @@ class PackedScene:
 # cube  : 6 planes = 270 (the reference re-transforms the ray per face)
 # cylinder: 33 + ~51 = 84
 # cone (extension): 33 + a, halfB, c (15) + discriminant (3) + base cap (~10) = 61
-FLOPS_PER_TEST = (52, 45, 270, 84, 61)
+# csg (extension): counted as one test of the composite; lower bound = its
+# bounding-sphere-culled leaf work is not modelled (0)
+FLOPS_PER_TEST = (52, 45, 270, 84, 61, 0)
 # Per shaded hit: surface props + ambient (21); per light: lighting (68).
 FLOPS_PER_SHADE = 21
 FLOPS_PER_LIGHT = 68

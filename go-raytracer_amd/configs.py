@@ -92,6 +92,28 @@ def c4(width=3840, height=2160):
                         width=width, height=height, file="c4.ppm", bg_start=BG0, bg_end=BG1)
 
 
+def c4csg(width=3840, height=2160):
+    """C4 as BASELINE.json states it: a cube with 64 subtracted spheres (4x4x4
+    lattice, r 0.2) -- GML `difference`, rendered as a CSG composite (contest
+    extension; the reference renderer rejects Difference, so parity-unpinned);
+    3840x2160, depth 8."""
+    cube = (S.Cube(S.material((0.9, 0.3, 0.3), 0.2, 0.0, 0.0, 0.0, 0.9, 0.4, 10.0))
+            .translate(-0.1, -0.6, 5.0).rotatey(30.0).rotatex(20.0).uscale(1.6).translate(-0.5, -0.5, -0.5))
+    glass = S.material((0.9, 1.0, 0.9), 0.2, 0.0, 0.8, 1.5, 0.5, 0.8, 60.0)
+    holes = None
+    for i in range(4):
+        for j in range(4):
+            for k in range(4):
+                sph = (S.Sphere(glass).translate(-0.1 + (i - 1.5) * 0.55, -0.6 + (j - 1.5) * 0.55,
+                                                 5.0 + (k - 1.5) * 0.55).uscale(0.2))
+                holes = sph if holes is None else S.union(holes, sph)
+    ground = S.Plane(S.material((0.6, 0.6, 0.7), 0.3, 0.0, 0.0, 0.0, 1.0, 0.0, 1.0)).translate(0.0, -2.0, 0.0)
+    sc = S.union(S.Difference(cube, holes), ground)
+    lights = [S.PointLight((4.0, 6.0, 0.0), (0.8, 0.8, 0.8)), S.PointLight((-6.0, 4.0, 2.0), (0.5, 0.5, 0.6))]
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=sc, depth=8, fov=90.0,
+                        width=width, height=height, file="c4csg.ppm", bg_start=BG0, bg_end=BG1)
+
+
 class _Pcg32:
     """Tiny deterministic generator for scene jitter (seed 2026); not on the path."""
 
@@ -128,7 +150,7 @@ def c5(width=7680, height=4320, nx=100, ny=100, nz=10):
                         width=width, height=height, file="c5.ppm", bg_start=BG0, bg_end=BG1)
 
 
-CONFIGS = {"canned": canned, "c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}
+CONFIGS = {"canned": canned, "c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5, "c4csg": c4csg}
 
 WORKLOADS = {
     "canned": "canned.gml 1900x1200 depth 7 (reference golden example_canned.png)",
@@ -137,4 +159,5 @@ WORKLOADS = {
     "c3": "cylinder + cube + sphere (cone substitute) over a reflective plane, 4 lights, 3840x2160, depth 6",
     "c4": "cube U 64 spheres (CSG substitute) + plane, 2 lights, 3840x2160, depth 8",
     "c5": "100k spheres + plane, 2 lights, 7680x4320, depth 8",
+    "c4csg": "cube minus 64 spheres (CSG difference, contest extension) + plane, 2 lights, 3840x2160, depth 8",
 }

@@ -106,8 +106,8 @@ enum { LDS_MAX_BYTES = RT_LDS_MAX };
 
 struct Params {
   int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
-  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_code, off_consts, off_entry,
-      blob_bytes;
+  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_csg, off_code, off_consts,
+      off_entry, blob_bytes;
   int lds_vm_off;     // LDS byte offset of the per-lane VM material records (LDS flavour)
   double* vm_global;  // per-lane VM material records (global flavour)
   const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
@@ -353,6 +353,179 @@ __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r,
       return cube_hit(l, t, face);
     default:  // RT_CYLINDER, RT_CONE
       return quadric_hit(l, t, face, k == RT_CONE);
+  }
+}
+
+// ---- CSG composites (contest extension; oracle/rt_oracle.c leaf_interval,
+// csg_member, csg_intersect restate the same semantics op for op) ----
+// One convex leaf's interval [a, b] along the ray and the faces it enters /
+// leaves by: f = fa | fb << 4 | 256 when non-empty.
+__device__ __forceinline__ void leaf_interval(int kind, const double* g, const Ray& r, double& a, double& b, int& f) {
+  const Ray l = to_obj(g, r);
+  a = -__builtin_inf();
+  b = __builtin_inf();
+  int fa = 0, fb = 0;
+  bool ok = true;
+  if (kind == RT_SPHERE) {
+    const double qa = dot(l.d, l.d), hb = dot(l.o, l.d), c = dot(l.o, l.o) - 1.0;
+    const double disc = hb * hb - qa * c;
+    if (disc < 0.0) {
+      ok = false;
+    } else {
+      const double sq = __builtin_sqrt(disc);
+      a = (-hb - sq) / qa;
+      b = (-hb + sq) / qa;
+    }
+  } else if (kind == RT_CUBE) {
+    const double o3[3] = {l.o.x, l.o.y, l.o.z}, d3v[3] = {l.d.x, l.d.y, l.d.z};
+    const int flo[3] = {2, 5, 0}, fhi[3] = {3, 4, 1};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (d3v[k] == 0.0) {
+        if (o3[k] < 0.0 || o3[k] > 1.0) ok = false;
+        continue;
+      }
+      const double ta = (0.0 - o3[k]) / d3v[k], tb = (1.0 - o3[k]) / d3v[k];
+      double lo = ta, hi = tb;
+      int fl = flo[k], fh = fhi[k];
+      if (d3v[k] < 0.0) {
+        lo = tb;
+        hi = ta;
+        fl = fhi[k];
+        fh = flo[k];
+      }
+      if (lo > a) {
+        a = lo;
+        fa = fl;
+      }
+      if (hi < b) {
+        b = hi;
+        fb = fh;
+      }
+    }
+    if (a > b) ok = false;
+  } else if (kind == RT_CYLINDER) {
+    const double qa = l.d.x * l.d.x + l.d.z * l.d.z;
+    if (qa > 1e-12) {
+      const double hb = l.o.x * l.d.x + l.o.z * l.d.z;
+      const double c0 = l.o.x * l.o.x + l.o.z * l.o.z - 1.0;
+      const double disc = hb * hb - qa * c0;
+      if (disc < 0.0) {
+        ok = false;
+      } else {
+        const double sq = __builtin_sqrt(disc);
+        a = (-hb - sq) / qa;
+        b = (-hb + sq) / qa;
+      }
+    } else if (l.o.x * l.o.x + l.o.z * l.o.z > 1.0) {
+      ok = false;
+    }
+    if (ok) {
+      if (__builtin_fabs(l.d.y) > 1e-12) {
+        const double tb0 = (0.0 - l.o.y) / l.d.y, tt = (1.0 - l.o.y) / l.d.y;
+        double lo = tb0, hi = tt;
+        int fl = 2, fh = 1;
+        if (l.d.y < 0.0) {
+          lo = tt;
+          hi = tb0;
+          fl = 1;
+          fh = 2;
+        }
+        if (lo > a) {
+          a = lo;
+          fa = fl;
+        }
+        if (hi < b) {
+          b = hi;
+          fb = fh;
+        }
+      } else if (l.o.y < 0.0 || l.o.y > 1.0) {
+        ok = false;
+      }
+      if (a > b) ok = false;
+    }
+  } else {  // RT_PLANE: the half-space n.p + D <= 0
+    const d3 n = mk(g[12], g[13], g[14]);
+    const double denom = dot(n, l.d);
+    if (__builtin_fabs(denom) < 1e-6) {
+      if (dot(n, l.o) + g[15] > 0.0) ok = false;
+    } else {
+      const double tt = (-g[15] - dot(n, l.o)) / denom;
+      if (denom < 0.0)
+        a = tt;
+      else
+        b = tt;
+    }
+  }
+  f = fa | (fb << 4) | (ok ? 256 : 0);
+}
+
+// Postfix membership of the composite just before (after = false) or just
+// after t (bit stacks, depth <= RT_CSG_MAX_LEAVES).
+__device__ __forceinline__ bool csg_member(const int* code, int n, const double* A, const double* B, const int* F,
+                                           double t, bool after) {
+  uint64_t st0 = 0, st1 = 0;
+  int sp = 0;
+  auto get = [&](int i) -> bool { return ((i < 64 ? st0 >> i : st1 >> (i - 64)) & 1) != 0; };
+  auto set = [&](int i, bool v) {
+    if (i < 64)
+      st0 = v ? (st0 | (1ull << i)) : (st0 & ~(1ull << i));
+    else
+      st1 = v ? (st1 | (1ull << (i - 64))) : (st1 & ~(1ull << (i - 64)));
+  };
+  for (int k = 0; k < n; k++) {
+    const int op = code[k];
+    if (op >= 0) {
+      const bool in = (F[op] & 256) && (after ? (A[op] <= t && t < B[op]) : (A[op] < t && t <= B[op]));
+      set(sp, in);
+      sp++;
+    } else {
+      sp -= 2;
+      const bool x = get(sp), y = get(sp + 1);
+      set(sp, op == RT_CSG_UNION ? (x || y) : (op == RT_CSG_INTERSECT ? (x && y) : (x && !y)));
+      sp++;
+    }
+  }
+  return (st0 & 1) != 0;
+}
+
+// Composite hit: the first leaf end point t > 0 (lowest leaf, entry first,
+// on ties) where membership changes. face = leaf << 4 | flip << 3 | leaf face.
+__device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, const int* code, int nobj,
+                                        const double* g, const Ray& r, double& t, int& face) {
+  const int* ci = reinterpret_cast<const int*>(g + 14);
+  const int first = nobj + ci[0], count = ci[1];
+  const int* prog = code + ci[2];
+  const int plen = ci[3];
+  double A[RT_CSG_MAX_LEAVES], B[RT_CSG_MAX_LEAVES];
+  int F[RT_CSG_MAX_LEAVES];
+  for (int j = 0; j < count; j++) leaf_interval(kinds[first + j], geo + (size_t)(first + j) * GEO, r, A[j], B[j], F[j]);
+  double tc = 0.0;
+  for (;;) {
+    double te = __builtin_inf();
+    int je = -1, jend = 0;
+    for (int j = 0; j < count; j++) {
+      if (!(F[j] & 256)) continue;
+      if (A[j] > tc && A[j] < te) {
+        te = A[j];
+        je = j;
+        jend = 0;
+      }
+      if (B[j] > tc && B[j] < te) {
+        te = B[j];
+        je = j;
+        jend = 1;
+      }
+    }
+    if (je < 0) return false;
+    const bool before = csg_member(prog, plen, A, B, F, te, false), after = csg_member(prog, plen, A, B, F, te, true);
+    if (before != after) {
+      const int flip = ((jend == 0) != after) ? 1 : 0;
+      t = te;
+      face = (je << 4) | (flip << 3) | (jend ? (F[je] >> 4) & 15 : F[je] & 15);
+      return true;
+    }
+    tc = te;
   }
 }
 
@@ -603,9 +776,10 @@ struct View {
   const int* kind;
   const int* objmat;
   const uint32_t* pref;  // [nobj + 1][PREF]: objects of each kind with index < i
+  const int* csg;        // CSG postfix programs (extension)
 };
 
-template <bool LDS, bool BVH>
+template <bool LDS, bool BVH, bool CSG>
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 3  // 168 VGPRs -> 3 waves/SIMD (C3 on par with 4; C2 -10%, C4 (BVH) -4%)
 #endif
@@ -632,6 +806,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   S.kind = reinterpret_cast<const int*>(base + P.off_kind);
   S.objmat = reinterpret_cast<const int*>(base + P.off_objmat);
   S.pref = reinterpret_cast<const uint32_t*>(base + P.off_pref);
+  S.csg = reinterpret_cast<const int*>(base + P.off_csg);
   S.code = reinterpret_cast<const uint32_t*>(base + P.off_code);
   S.entry = reinterpret_cast<const int*>(base + P.off_entry);
   S.consts = reinterpret_cast<const uint64_t*>(base + P.off_consts);
@@ -879,7 +1054,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if (test) {
           double t;
           int f;
-          if (object_hit(k, g, ray, t, f)) {
+          bool h;
+          if constexpr (CSG)
+            h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, ray, t, f) : object_hit(k, g, ray, t, f);
+          else
+            h = object_hit(k, g, ray, t, f);
+          if (h) {
             if (!found || t < best_t || (BVH && t == best_t && i < best_i)) {
               found = true;
               best_t = t;
@@ -892,9 +1072,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if constexpr (!BVH) {
         for (int i = 0; i < P.nobj; i++) trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
       } else {
-        for (int p = 0; p < P.nplanes; p++) {
+        for (int p = 0; p < P.nplanes; p++) {  // unbounded objects: planes, unbounded CSG
           const int i = P.planes[p];
-          trace_obj(i, RT_PLANE, S.geo + (size_t)i * GEO, tr);
+          trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
         }
         const F3 idf = f3_rcp(df);
 #ifdef RT_PHASE_TIMING
@@ -974,9 +1154,19 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     int mat = 0;
     bool surf_bad = false;
     if (hit) {
-      const double* g = S.geo + (size_t)hit_i * GEO;
-      const double* s = S.shade + (size_t)hit_i * SHD;
-      const int k = S.kind[hit_i];
+      int si = hit_i, sf = hit_f;  // the surface: the object, or a CSG composite's leaf
+      bool flip = false;
+      if constexpr (CSG) {
+        if (S.kind[hit_i] == RT_CSG) {
+          const int* ci = reinterpret_cast<const int*>(S.geo + (size_t)hit_i * GEO + 14);
+          si = P.nobj + ci[0] + (hit_f >> 4);
+          flip = ((hit_f >> 3) & 1) != 0;
+          sf = hit_f & 7;
+        }
+      }
+      const double* g = S.geo + (size_t)si * GEO;
+      const double* s = S.shade + (size_t)si * SHD;
+      const int k = S.kind[si];
       Ray l = to_obj(g, ray);
       d3 p = add(l.o, scale(l.d, hit_t));  // Hit.PointObj
       pw = mk(s[0] * p.x + s[1] * p.y + s[2] * p.z + s[3], s[4] * p.x + s[5] * p.y + s[6] * p.z + s[7],
@@ -984,26 +1174,26 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if (k == RT_SPHERE) {
         nw = p;
       } else if (k == RT_CYLINDER || k == RT_CONE) {
-        d3 n = hit_f == 0 ? (k == RT_CONE ? mk(p.x, -p.y, p.z) : mk(p.x, 0, p.z))
-                          : (hit_f == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
+        d3 n = sf == 0 ? (k == RT_CONE ? mk(p.x, -p.y, p.z) : mk(p.x, 0, p.z)) : (sf == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
         // NormalMat = WorldToObject^T (raytracer.go:814): MulDir then Normalize.
         nw = norm(mk(g[0] * n.x + g[4] * n.y + g[8] * n.z, g[1] * n.x + g[5] * n.y + g[9] * n.z,
                      g[2] * n.x + g[6] * n.y + g[10] * n.z));
       } else {
-        nw = mk(s[12 + hit_f * 3], s[13 + hit_f * 3], s[14 + hit_f * 3]);
+        nw = mk(s[12 + sf * 3], s[13 + sf * 3], s[14 + sf * 3]);
       }
-      mat = S.objmat[(size_t)hit_i * OMAT + hit_f];
+      if (flip) nw = neg(nw);  // the composite's outward normal
+      mat = S.objmat[(size_t)si * OMAT + sf];
       if (mat < 0) {
         // Closure surface: (face, u, v) as ComputeSurfaceProps computes them
         // (raytracer.go:124-150, 196-205, 249, 339-359), then the VM.
         double u, v;
         bool bad = false;
-        long long face = (k == RT_PLANE) ? 0 : hit_f;
+        long long face = (k == RT_PLANE) ? 0 : sf;
         if (k == RT_SPHERE) {
           bad = __builtin_fabs(p.y) > 1;
           v = (p.y + 1.0) / 2.0;
           u = go_acos(p.z / __builtin_sqrt(1.0 - p.y * p.y)) / 6.283185307179586;
-        } else if ((k == RT_CYLINDER || k == RT_CONE) && hit_f == 0) {
+        } else if ((k == RT_CYLINDER || k == RT_CONE) && sf == 0) {
           u = (go_atan2(p.x, p.z) + 3.141592653589793) / 6.283185307179586;
           v = p.y;
         } else {
@@ -1083,7 +1273,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           if (test) {
             double t;
             int f;
-            if (object_hit(k, g, sr, t, f)) {
+            bool h;
+            if constexpr (CSG)
+              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f) : object_hit(k, g, sr, t, f);
+            else
+              h = object_hit(k, g, sr, t, f);
+            if (h) {
               if (t * rlen < dist) {
                 open = false;
                 send = i + 1;
@@ -1106,14 +1301,19 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           if (test) {
             double t;
             int f;
-            if (object_hit(k, g, sr, t, f)) {
+            bool h;
+            if constexpr (CSG)
+              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f) : object_hit(k, g, sr, t, f);
+            else
+              h = object_hit(k, g, sr, t, f);
+            if (h) {
               if (t * rlen < dist) occ = i;
             }
           }
         };
         for (int p = 0; p < P.nplanes; p++) {
           const int i = P.planes[p];
-          shadow_obj(i, RT_PLANE, S.geo + (size_t)i * GEO, hit);
+          shadow_obj(i, S.kind[i], S.geo + (size_t)i * GEO, hit);
         }
         const F3 sidf = f3_rcp(sdf);
 #ifdef RT_PHASE_TIMING
@@ -1171,7 +1371,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         sc1 += pe.y - (hk == 1 ? 1u : 0u);
         sc2 += pe.z - (hk == 2 ? 1u : 0u);
         sc3 += pe.w - (hk == 3 ? 1u : 0u);
-        if (P.kind_mask & 16) cnt_add(CNT_ST0 + 4, pe4 - (hk == 4 ? 1u : 0u));  // cones: rare, flushed per light
+        if (P.kind_mask & 16) cnt_add(CNT_ST0 + 4, pe4 - (hk == 4 ? 1u : 0u));  // cones, CSG: rare, flushed per light
+        if (P.kind_mask & 32) cnt_add(CNT_ST0 + 5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
       }
       PH_MARK(4);
       if (hit && open) {
@@ -1322,10 +1523,14 @@ __global__ void rt_debug_vm_kernel(const char* __restrict__ blob, int off_code, 
   err[i] = run_vm(code, consts, entry[prog], face[i], u[i], v[i], out + (size_t)i * 10) ? 1 : 0;
 }
 
-template __global__ void rt_render_kernel<true, false>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<false, false>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<true, true>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<false, true>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<true, false, false>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<false, false, false>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<true, true, false>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<false, true, false>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<true, false, true>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<false, false, true>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<true, true, true>(const char* __restrict__, Params);
+template __global__ void rt_render_kernel<false, true, true>(const char* __restrict__, Params);
 // ===========================================================================
 // Host side: scene conversion (raytracer.go:724-830) and the C ABI
 // ===========================================================================
@@ -1481,7 +1686,9 @@ struct DevScene {
   double amb[3] = {0, 0, 0}, bg0[3] = {0, 0, 0}, bg1[3] = {0, 0, 0};
   char* blob = nullptr;
   int blob_bytes = 0;
-  int off_geo = 0, off_shade = 0, off_mats = 0, off_lights = 0, off_kind = 0, off_objmat = 0, off_prefb = 0;
+  int off_geo = 0, off_shade = 0, off_mats = 0, off_lights = 0, off_kind = 0, off_objmat = 0, off_prefb = 0,
+      off_csg = 0;
+  bool has_csg = false;
   std::vector<int> kinds;  // host copy for the per-kind test counts
   int off_code = 0, off_consts = 0, off_entry = 0, num_programs = 0;
   // BVH flavour: one device buffer nodes | leaf objects | planes | prefix counts
@@ -1666,12 +1873,12 @@ int rt_create(int device, rt_context** out) {
   // Persistent grids: as many workgroups as are resident (any extra block just
   // finds the queue drained). The LDS flavour is sized for the LDS budget.
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true, false>, WG, LDS_MAX_BYTES) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true, false, false>, WG, LDS_MAX_BYTES) !=
           hipSuccess || per_cu <= 0)
     per_cu = 2;
   c->grid_lds = c->cus * std::min(per_cu, 8);
   per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false, false>, WG, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false, false, false>, WG, 0) != hipSuccess ||
       per_cu <= 0)
     per_cu = 2;
   c->grid_glb = c->cus * std::min(per_cu, 8);
@@ -1754,13 +1961,41 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   s.nlights = ext_lights ? in->num_ext_lights : in->num_lights;
   s.nmats = in->num_materials;
 
-  std::vector<double> geo((size_t)s.nobj * GEO, 0.0), shade((size_t)s.nobj * SHD, 0.0);
-  std::vector<int> kind(s.nobj), objmat((size_t)s.nobj * OMAT, 0);
-  std::vector<double> bcen((size_t)s.nobj * 3, 0.0), brad((size_t)s.nobj, 0.0);  // padded bounding spheres
-  for (int i = 0; i < s.nobj; i++) {
-    const rt_object& o = in->objects[i];
+  // CSG composites (extension): their leaves follow the top-level objects in
+  // every per-object array (index nobj + leaf).
+  const int nleaves = std::max(0, in->num_csg_leaves), ncsg = std::max(0, in->csg_code_words);
+  if ((nleaves && !in->csg_leaves) || (ncsg && !in->csg_code)) return fail(RT_E_INVALID, "CSG arrays are NULL");
+  const int ntot = s.nobj + nleaves;
+  std::vector<double> geo((size_t)ntot * GEO, 0.0), shade((size_t)ntot * SHD, 0.0);
+  std::vector<int> kind(ntot), objmat((size_t)ntot * OMAT, 0);
+  std::vector<double> bcen((size_t)ntot * 3, 0.0), brad((size_t)ntot, 0.0);  // padded bounding spheres
+  for (int i = 0; i < ntot; i++) {
+    const bool leaf = i >= s.nobj;
+    const rt_object& o = leaf ? in->csg_leaves[i - s.nobj] : in->objects[i];
     if (o.kind < 0 || o.kind >= RT_NUM_KINDS) return fail(RT_E_INVALID, "unknown scene object type");
+    if (leaf && o.kind != RT_SPHERE && o.kind != RT_CUBE && o.kind != RT_CYLINDER && o.kind != RT_PLANE)
+      return fail(RT_E_INVALID, "CSG leaves are spheres, cubes, cylinders or planes");
     kind[i] = o.kind;
+    if (o.kind == RT_CSG) {  // validated program; geometry filled in below
+      if (o.csg_count <= 0 || o.csg_count > RT_CSG_MAX_LEAVES || o.csg_first < 0 ||
+          o.csg_first + o.csg_count > nleaves || o.csg_code < 0 || o.csg_code_len <= 0 ||
+          o.csg_code + o.csg_code_len > ncsg)
+        return fail(RT_E_INVALID, "CSG composite: leaf / program range");
+      int depth = 0;
+      for (int k = 0; k < o.csg_code_len; k++) {
+        const int op = in->csg_code[o.csg_code + k];
+        if (op >= 0) {
+          if (op >= o.csg_count) return fail(RT_E_INVALID, "CSG program: leaf index");
+          depth++;
+        } else {
+          if (op < RT_CSG_DIFFERENCE || depth < 2) return fail(RT_E_INVALID, "CSG program: operator");
+          depth--;
+        }
+        if (depth > RT_CSG_MAX_LEAVES) return fail(RT_E_INVALID, "CSG program: depth");
+      }
+      if (depth != 1) return fail(RT_E_INVALID, "CSG program: does not reduce to one solid");
+      continue;
+    }
     for (int f = 0; f < RT_MAX_FACES; f++) {
       if (o.material[f] >= in->num_materials || o.material[f] < -std::max(0, in->num_programs))
         return fail(RT_E_INVALID, "material / surface program index out of range");
@@ -1838,6 +2073,71 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
         for (int k = 0; k < 3; k++) sh[12 + f * 3 + k] = nw[k];
       }
     }
+  }
+  // CSG composites: bounding sphere from the leaves (union: enclosing sphere,
+  // intersect: the smaller operand, difference: the left operand; a plane leaf
+  // is unbounded), leaf range and program in geo slots 14..15.
+  for (int i = 0; i < s.nobj; i++) {
+    if (kind[i] != RT_CSG) continue;
+    const rt_object& o = in->objects[i];
+    struct Bd {
+      double c[3], r;
+      bool fin;
+    };
+    std::vector<Bd> st;
+    for (int k = 0; k < o.csg_code_len; k++) {
+      const int op = in->csg_code[o.csg_code + k];
+      if (op >= 0) {
+        const int li = s.nobj + o.csg_first + op;
+        Bd b;
+        b.fin = kind[li] != RT_PLANE;
+        for (int q = 0; q < 3; q++) b.c[q] = bcen[(size_t)li * 3 + q];
+        b.r = brad[li];
+        st.push_back(b);
+        continue;
+      }
+      const Bd y = st.back();
+      st.pop_back();
+      const Bd x = st.back();
+      st.pop_back();
+      Bd r = x;
+      if (op == RT_CSG_UNION) {
+        if (!x.fin || !y.fin) {
+          r.fin = false;
+        } else {
+          const double d = std::sqrt((y.c[0] - x.c[0]) * (y.c[0] - x.c[0]) + (y.c[1] - x.c[1]) * (y.c[1] - x.c[1]) +
+                                     (y.c[2] - x.c[2]) * (y.c[2] - x.c[2]));
+          if (d + y.r <= x.r) {
+            r = x;
+          } else if (d + x.r <= y.r) {
+            r = y;
+          } else {
+            r.r = (d + x.r + y.r) / 2.0;
+            for (int q = 0; q < 3; q++) r.c[q] = x.c[q] + (y.c[q] - x.c[q]) * ((r.r - x.r) / d);
+            r.r = r.r * 1.0001 + 1e-9;
+          }
+        }
+      } else if (op == RT_CSG_INTERSECT) {
+        r = !x.fin ? y : (!y.fin ? x : (y.r < x.r ? y : x));
+      }  // difference: the left operand's bound
+      st.push_back(r);
+    }
+    double* g = &geo[(size_t)i * GEO];
+    float* b = reinterpret_cast<float*>(&g[12]);
+    if (st.back().fin) {
+      for (int q = 0; q < 3; q++) b[q] = (float)st.back().c[q];
+      b[3] = f_up(st.back().r + 1e-4 * (1.0 + std::fabs(st.back().c[0]) + std::fabs(st.back().c[1]) +
+                                         std::fabs(st.back().c[2])));
+    } else {
+      b[0] = b[1] = b[2] = 0.0f;
+      b[3] = std::numeric_limits<float>::infinity();  // never culled
+    }
+    int* ci = reinterpret_cast<int*>(&g[14]);
+    ci[0] = o.csg_first;
+    ci[1] = o.csg_count;
+    ci[2] = o.csg_code;
+    ci[3] = o.csg_code_len;
+    s.has_csg = true;
   }
   std::vector<double> mats((size_t)s.nmats * MAT, 0.0);
   for (int m = 0; m < s.nmats; m++) {
@@ -1949,7 +2249,8 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     prefb[(size_t)(i + 1) * PREF + kind[i]]++;
   }
   s.off_prefb = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
-  s.off_code = align16(s.off_prefb + (int)(prefb.size() * sizeof(uint32_t)));
+  s.off_csg = align16(s.off_prefb + (int)(prefb.size() * sizeof(uint32_t)));
+  s.off_code = align16(s.off_csg + ncsg * (int)sizeof(int));
   s.off_consts = align16(s.off_code + ncode * (int)sizeof(uint32_t));
   s.off_entry = align16(s.off_consts + nconst * (int)sizeof(uint64_t));
   s.blob_bytes = align16(s.off_entry + nprog * (int)sizeof(int));
@@ -1962,6 +2263,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     std::memcpy(blob.data() + s.off_kind, kind.data(), kind.size() * sizeof(int));
     std::memcpy(blob.data() + s.off_objmat, objmat.data(), objmat.size() * sizeof(int));
     std::memcpy(blob.data() + s.off_prefb, prefb.data(), prefb.size() * sizeof(uint32_t));
+    if (ncsg) std::memcpy(blob.data() + s.off_csg, in->csg_code, (size_t)ncsg * sizeof(int));
     if (nprog) {
       std::memcpy(blob.data() + s.off_code, in->program_code, (size_t)ncode * sizeof(uint32_t));
       std::memcpy(blob.data() + s.off_consts, in->program_consts, (size_t)nconst * sizeof(uint64_t));
@@ -1973,11 +2275,11 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       return rc;
     }
   }
-  s.kinds = kind;
+  s.kinds.assign(kind.begin(), kind.begin() + s.nobj);  // top-level objects (test counts)
   {
     // Acceleration buffer: [BVH nodes | leaf objects] | planes.
     std::vector<int> bounded, planes;
-    for (int i = 0; i < s.nobj; i++) (kind[i] == RT_PLANE ? planes : bounded).push_back(i);
+    for (int i = 0; i < s.nobj; i++) (kind[i] == RT_PLANE || kind[i] == RT_CSG ? planes : bounded).push_back(i);
     BvhBuild b;
     if ((int)bounded.size() >= RT_BVH_MIN) {
       b.c = &bcen;
@@ -2055,8 +2357,13 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
   const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * 12 : 0);
   const int shmem = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
-  const void* kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true> : (const void*)rt_render_kernel<true, false>)
-                        : (s.use_bvh ? (const void*)rt_render_kernel<false, true> : (const void*)rt_render_kernel<false, false>);
+  const void* kfn;
+  if (s.has_csg)
+    kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, true> : (const void*)rt_render_kernel<true, false, true>)
+              : (s.use_bvh ? (const void*)rt_render_kernel<false, true, true> : (const void*)rt_render_kernel<false, false, true>);
+  else
+    kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, false> : (const void*)rt_render_kernel<true, false, false>)
+              : (s.use_bvh ? (const void*)rt_render_kernel<false, true, false> : (const void*)rt_render_kernel<false, false, false>);
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, WG, shmem) != hipSuccess) per_cu = 0;
   if (per_cu <= 0) per_cu = 1;
@@ -2072,6 +2379,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.off_kind = s.off_kind;
   P.off_objmat = s.off_objmat;
   P.off_pref = s.off_prefb;
+  P.off_csg = s.off_csg;
   P.off_code = s.off_code;
   P.off_consts = s.off_consts;
   P.off_entry = s.off_entry;
@@ -2112,14 +2420,19 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   HIP_TRY(hipMemsetAsync(c->queue, 0, 256, st));
   HIP_TRY(hipEventRecord(c->ev0, st));
   const char* blob = s.blob;
-  if (lds && s.use_bvh)
-    hipLaunchKernelGGL((rt_render_kernel<true, true>), dim3(grid), dim3(WG), shmem, st, blob, P);
-  else if (lds)
-    hipLaunchKernelGGL((rt_render_kernel<true, false>), dim3(grid), dim3(WG), shmem, st, blob, P);
-  else if (s.use_bvh)
-    hipLaunchKernelGGL((rt_render_kernel<false, true>), dim3(grid), dim3(WG), shmem, st, blob, P);
-  else
-    hipLaunchKernelGGL((rt_render_kernel<false, false>), dim3(grid), dim3(WG), shmem, st, blob, P);
+#define RT_LAUNCH(L, B, Cs) hipLaunchKernelGGL((rt_render_kernel<L, B, Cs>), dim3(grid), dim3(WG), shmem, st, blob, P)
+  if (s.has_csg) {
+    if (lds && s.use_bvh) RT_LAUNCH(true, true, true);
+    else if (lds) RT_LAUNCH(true, false, true);
+    else if (s.use_bvh) RT_LAUNCH(false, true, true);
+    else RT_LAUNCH(false, false, true);
+  } else {
+    if (lds && s.use_bvh) RT_LAUNCH(true, true, false);
+    else if (lds) RT_LAUNCH(true, false, false);
+    else if (s.use_bvh) RT_LAUNCH(false, true, false);
+    else RT_LAUNCH(false, false, false);
+  }
+#undef RT_LAUNCH
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   c->timed = true;

@@ -255,7 +255,7 @@ def _closure(e):
     return e.pop_t(VClosure, "gml.VClosure")
 
 
-_SCENE_TYPES = (S.Sphere, S.Cube, S.Cylinder, S.Plane, S.Union, S.Difference, S.Cone)
+_SCENE_TYPES = (S.Sphere, S.Cube, S.Cylinder, S.Plane, S.Union, S.Difference, S.Cone, S.Intersect)
 
 
 def _sceneobj(e):
@@ -626,4 +626,11 @@ def b_real(e):
     e.stack.append(VReal(float(int(_int(e)))))
 
 
-EXT_BUILTINS = {"cone": b_cone, "light": b_light, "spotlight": b_spotlight, "real": b_real}
+def b_intersect(e):
+    """`s1 s2 intersect`: the solid in both (argument order as `difference`)."""
+    a, b = _pop2(e, _sceneobj)
+    e.stack.append(S.Intersect(a, b))
+
+
+EXT_BUILTINS = {"cone": b_cone, "light": b_light, "spotlight": b_spotlight, "real": b_real,
+                "intersect": b_intersect}

@@ -157,13 +157,24 @@ def union(first, second):
 
 @dataclass(frozen=True)
 class Difference(SceneObject):
-    """gml.Difference (evaluator.go:264-287). The reference renderer rejects it
-    (raytracer.go:825-826) and so does convert()."""
+    """gml.Difference (evaluator.go:264-287): solid a minus solid b. The
+    reference renderer rejects it (raytracer.go:825-826); here it renders as a
+    CSG composite (contest extension, parity-unpinned; include/rt_abi.h RT_CSG)."""
     a: object = None
     b: object = None
 
     def transform(self, mat):
         return Difference(self.a.transform(mat), self.b.transform(mat))
+
+
+@dataclass(frozen=True)
+class Intersect(SceneObject):
+    """GML `intersect` (contest extension, not in the reference): a and b."""
+    a: object = None
+    b: object = None
+
+    def transform(self, mat):
+        return Intersect(self.a.transform(mat), self.b.transform(mat))
 
 
 @dataclass
@@ -190,18 +201,51 @@ _KIND = {Sphere: abi.RT_SPHERE, Plane: abi.RT_PLANE, Cube: abi.RT_CUBE, Cylinder
 
 
 def flatten(root):
-    """BFS union flattening, raytracer.go:776-828 (order decides closestHit ties)."""
+    """BFS union flattening, raytracer.go:776-828 (order decides closestHit ties).
+    A Difference / Intersect is kept whole: one CSG composite (extension)."""
     out = []
     queue = [root]
     while queue:
         obj = queue.pop(0)
         if isinstance(obj, Union):
             queue.extend(obj.objects)
-        elif type(obj) in _KIND:
+        elif type(obj) in _KIND or isinstance(obj, (Difference, Intersect)):
             out.append(obj)
         else:
             raise TypeError("unknown scene object type %s" % type(obj).__name__)
     return out
+
+
+_CSG_LEAF = (Sphere, Cube, Cylinder, Plane)
+
+
+def csg_program(obj):
+    """Leaves (in order) and the postfix program of a CSG composite: unions
+    inside a composite are set unions (include/rt_abi.h RT_CSG)."""
+    leaves, code = [], []
+
+    def walk(o):
+        if isinstance(o, Union):
+            if not o.objects:
+                raise ValueError("empty union inside a CSG composite")
+            walk(o.objects[0])
+            for c in o.objects[1:]:
+                walk(c)
+                code.append(abi.RT_CSG_UNION)
+        elif isinstance(o, (Difference, Intersect)):
+            walk(o.a)
+            walk(o.b)
+            code.append(abi.RT_CSG_DIFFERENCE if isinstance(o, Difference) else abi.RT_CSG_INTERSECT)
+        elif isinstance(o, _CSG_LEAF):
+            code.append(len(leaves))
+            leaves.append(o)
+        else:
+            raise ValueError("%s cannot be a CSG leaf" % type(o).__name__)
+
+    walk(obj)
+    if len(leaves) > abi.RT_CSG_MAX_LEAVES:
+        raise ValueError("CSG composite with %d leaves (max %d)" % (len(leaves), abi.RT_CSG_MAX_LEAVES))
+    return leaves, code
 
 
 def _face_materials(obj, kind):
@@ -244,10 +288,8 @@ def convert(args: RenderArgs) -> abi.PackedScene:
             programs.append((sf, compile_surface(sf, stack)))
         return -(prog_index[key] + 1)
 
-    c_objs = (abi.rt_object * max(1, len(objs)))()
-    for i, o in enumerate(objs):
+    def fill(co, o):
         kind = _KIND[type(o)]
-        co = c_objs[i]
         co.kind = kind
         fm = _face_materials(o, kind)
         idx = [midx(m) if isinstance(m, Material) else pidx(m) for m in fm]
@@ -264,6 +306,25 @@ def convert(args: RenderArgs) -> abi.PackedScene:
             for k in range(3):
                 co.plane_point[k] = float(o.point[k])
                 co.plane_normal[k] = float(o.normal[k])
+
+    c_objs = (abi.rt_object * max(1, len(objs)))()
+    csg_leaves, csg_code = [], []
+    for i, o in enumerate(objs):
+        co = c_objs[i]
+        if isinstance(o, (Difference, Intersect)):
+            leaves, code = csg_program(o)
+            co.kind = abi.RT_CSG
+            co.csg_first, co.csg_count = len(csg_leaves), len(leaves)
+            co.csg_code, co.csg_code_len = len(csg_code), len(code)
+            csg_leaves.extend(leaves)
+            csg_code.extend(code)
+        else:
+            fill(co, o)
+    c_leaves = None
+    if csg_leaves:
+        c_leaves = (abi.rt_object * len(csg_leaves))()
+        for j, o in enumerate(csg_leaves):
+            fill(c_leaves[j], o)
     if not mats:
         mats.append(Material())
     c_mats = (abi.rt_material * len(mats))()
@@ -327,6 +388,13 @@ def convert(args: RenderArgs) -> abi.PackedScene:
     sc.materials = C.cast(c_mats, C.POINTER(abi.rt_material))
     sc.num_objects = len(objs)
     sc.num_materials = len(mats)
+    c_code = None
+    if csg_leaves:
+        c_code = (C.c_int32 * len(csg_code))(*csg_code)
+        sc.csg_leaves = C.cast(c_leaves, C.POINTER(abi.rt_object))
+        sc.csg_code = C.cast(c_code, C.POINTER(C.c_int32))
+        sc.num_csg_leaves = len(csg_leaves)
+        sc.csg_code_words = len(csg_code)
     packed_progs = None
     if programs:
         from .gml.surface_compiler import OP
@@ -350,4 +418,6 @@ def convert(args: RenderArgs) -> abi.PackedScene:
         sc.program_code_words = len(words)
         sc.program_const_count = len(consts)
         packed_progs = (c_code, c_consts, c_entry, [sf for sf, _ in programs], args.state)
-    return abi.PackedScene(sc, c_lights, c_objs, c_mats, packed_progs, c_ext)
+    packed = abi.PackedScene(sc, c_lights, c_objs, c_mats, packed_progs, c_ext)
+    packed._csg = (c_leaves, c_code)
+    return packed

@@ -52,7 +52,20 @@ extern "C" {
  * parity-unpinned): apex at the origin, x^2 + z^2 = y^2 for 0 <= y <= 1,
  * base disk at y = 1. Faces 0 side, 1 base. */
 #define RT_CONE 4
-#define RT_NUM_KINDS 5
+/* Contest extension (GML `intersect` / `difference`; the reference renderer
+ * rejects Difference, raytracer.go:825-826): one composite solid. Its leaves
+ * are rt_scene.csg_leaves[csg_first .. csg_first + csg_count) (spheres, cubes,
+ * cylinders, planes as half-spaces n.p + D <= 0) combined by a postfix program
+ * rt_scene.csg_code[csg_code .. csg_code + csg_code_len): v >= 0 pushes leaf v
+ * (relative to csg_first), RT_CSG_UNION / _INTERSECT / _DIFFERENCE pop two.
+ * The hit is the first interval end point t > 0 at which the composite's
+ * membership changes (oracle/rt_oracle.c csg_intersect). */
+#define RT_CSG 5
+#define RT_NUM_KINDS 6
+#define RT_CSG_UNION (-1)
+#define RT_CSG_INTERSECT (-2)
+#define RT_CSG_DIFFERENCE (-3)
+#define RT_CSG_MAX_LEAVES 128
 
 #define RT_MAX_FACES 6 /* prim.NUM_CUBE_SIDES, internal/prim/plane.go:27 */
 
@@ -122,6 +135,8 @@ typedef struct rt_object {
     double transform[16];
     double plane_point[3];
     double plane_normal[3];
+    /* RT_CSG only (see RT_CSG) */
+    int32_t csg_first, csg_count, csg_code, csg_code_len;
 } rt_object;
 
 /* gml.RenderArgs (internal/gml/evaluator.go:14-28) with the scene already
@@ -156,6 +171,11 @@ typedef struct rt_scene {
     const rt_light *ext_lights;
     int32_t num_ext_lights;
     int32_t reserved1;
+    /* ABI 2: CSG composites (RT_CSG objects) */
+    const rt_object *csg_leaves;
+    const int32_t *csg_code;
+    int32_t num_csg_leaves;
+    int32_t csg_code_words;
 } rt_scene;
 
 /* Work counters, identical in the CPU oracle and the GPU path.

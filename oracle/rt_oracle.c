@@ -104,6 +104,7 @@ typedef struct {
     int material[RT_MAX_FACES];
     mat4 o2w, w2o, normal_mat;
     plane_face face[RT_MAX_FACES]; /* plane: face[0]; cube: 6 faces */
+    int csg_first, csg_count, csg_code, csg_code_len; /* RT_CSG (extension) */
 } object;
 
 typedef struct {
@@ -120,6 +121,9 @@ typedef struct {
     double *lcos, *lexp;
     int nobj;
     object *obj;
+    int nleaves, ncode;       /* CSG extension: leaves and postfix programs */
+    object *leaves;
+    const int32_t *code;
     const rt_material *mats;
     int nmats;
 } scene;
@@ -269,6 +273,140 @@ static int cone_intersect(const object *o, ray r, double *t, vec3 *p, int *face)
     return 1;
 }
 
+/* ---- CSG (contest extension; not in the reference, parity-unpinned) ----
+ * Each leaf is a convex solid whose intersection with the (object-space) ray
+ * is one interval [a, b] with the faces it enters / leaves by. A plane is the
+ * half-space n.p + D <= 0. The composite's hit is the first end point t > 0 of
+ * any leaf interval (lowest leaf index, entry before exit, on ties) where the
+ * postfix membership formula changes between just before and just after t. */
+typedef struct { double a, b; int fa, fb, ok; } interval;
+
+static interval leaf_interval(const object *o, ray r) {
+    interval iv = {-INFINITY, INFINITY, 0, 0, 1};
+    ray lr = to_object(r, &o->w2o);
+    vec3 O = lr.origin, D = lr.dir;
+    switch (o->kind) {
+    case RT_SPHERE: {  /* sphere_intersect's quadratic, both roots */
+        double a = v_dot(D, D), hb = v_dot(O, D), c = v_dot(O, O) - 1.0;
+        double disc = hb * hb - a * c;
+        if (disc < 0.0) { iv.ok = 0; break; }
+        double sq = sqrt(disc);
+        iv.a = (-hb - sq) / a;
+        iv.b = (-hb + sq) / a;
+        break;
+    }
+    case RT_CUBE: {  /* slabs [0, 1]^3; faces prim.CubeSide (plane.go:14-25) */
+        const double o3[3] = {O.x, O.y, O.z}, d3v[3] = {D.x, D.y, D.z};
+        const int flo[3] = {2, 5, 0}, fhi[3] = {3, 4, 1};
+        for (int k = 0; k < 3; k++) {
+            if (d3v[k] == 0.0) {
+                if (o3[k] < 0.0 || o3[k] > 1.0) iv.ok = 0;
+                continue;
+            }
+            double ta = (0.0 - o3[k]) / d3v[k], tb = (1.0 - o3[k]) / d3v[k];
+            double lo = ta, hi = tb;
+            int fl = flo[k], fh = fhi[k];
+            if (d3v[k] < 0.0) { lo = tb; hi = ta; fl = fhi[k]; fh = flo[k]; }
+            if (lo > iv.a) { iv.a = lo; iv.fa = fl; }
+            if (hi < iv.b) { iv.b = hi; iv.fb = fh; }
+        }
+        if (iv.a > iv.b) iv.ok = 0;
+        break;
+    }
+    case RT_CYLINDER: {  /* side (face 0), caps top 1 / bottom 2 */
+        double a = D.x * D.x + D.z * D.z;
+        if (a > 1e-12) {
+            double hb = O.x * D.x + O.z * D.z;
+            double c0 = O.x * O.x + O.z * O.z - 1.0;
+            double disc = hb * hb - a * c0;
+            if (disc < 0.0) { iv.ok = 0; break; }
+            double sq = sqrt(disc);
+            iv.a = (-hb - sq) / a;
+            iv.b = (-hb + sq) / a;
+        } else if (O.x * O.x + O.z * O.z > 1.0) {
+            iv.ok = 0;
+            break;
+        }
+        if (fabs(D.y) > 1e-12) {
+            double tb0 = (0.0 - O.y) / D.y, tt = (1.0 - O.y) / D.y;
+            double lo = tb0, hi = tt;
+            int fl = 2, fh = 1;
+            if (D.y < 0.0) { lo = tt; hi = tb0; fl = 1; fh = 2; }
+            if (lo > iv.a) { iv.a = lo; iv.fa = fl; }
+            if (hi < iv.b) { iv.b = hi; iv.fb = fh; }
+        } else if (O.y < 0.0 || O.y > 1.0) {
+            iv.ok = 0;
+            break;
+        }
+        if (iv.a > iv.b) iv.ok = 0;
+        break;
+    }
+    case RT_PLANE: {  /* half-space below the plane; plane_intersect_obj's t */
+        const plane_face *f = &o->face[0];
+        double denom = v_dot(f->normal, D);
+        if (fabs(denom) < 1e-6) {
+            if (v_dot(f->normal, O) + f->d > 0.0) iv.ok = 0;
+            break;
+        }
+        double tt = (-f->d - v_dot(f->normal, O)) / denom;
+        if (denom < 0.0) iv.a = tt;
+        else iv.b = tt;
+        break;
+    }
+    default:
+        iv.ok = 0;
+    }
+    return iv;
+}
+
+static int csg_member(const scene *s, const object *o, const interval *iv, double t, int after) {
+    unsigned long long st[2] = {0, 0};  /* bit stack, depth <= RT_CSG_MAX_LEAVES */
+    int sp = 0;
+    for (int k = 0; k < o->csg_code_len; k++) {
+        int op = s->code[o->csg_code + k];
+        if (op >= 0) {
+            const interval *v = &iv[op];
+            int in = v->ok && (after ? (v->a <= t && t < v->b) : (v->a < t && t <= v->b));
+            if (in) st[sp >> 6] |= 1ULL << (sp & 63); else st[sp >> 6] &= ~(1ULL << (sp & 63));
+            sp++;
+        } else {
+            sp -= 2;
+            int x = (int)((st[sp >> 6] >> (sp & 63)) & 1), y = (int)((st[(sp + 1) >> 6] >> ((sp + 1) & 63)) & 1);
+            int r = op == RT_CSG_UNION ? (x | y) : (op == RT_CSG_INTERSECT ? (x & y) : (x & !y));
+            if (r) st[sp >> 6] |= 1ULL << (sp & 63); else st[sp >> 6] &= ~(1ULL << (sp & 63));
+            sp++;
+        }
+    }
+    return (int)(st[0] & 1);
+}
+
+/* face out: leaf << 4 | flip << 3 | leaf face; *p = the leaf's object point */
+static int csg_intersect(const scene *s, const object *o, ray r, double *t, vec3 *p, int *face) {
+    interval iv[RT_CSG_MAX_LEAVES];
+    for (int j = 0; j < o->csg_count; j++) iv[j] = leaf_interval(&s->leaves[o->csg_first + j], r);
+    double tc = 0.0;
+    for (;;) {
+        double te = INFINITY;
+        int je = -1, jend = 0;
+        for (int j = 0; j < o->csg_count; j++) {
+            if (!iv[j].ok) continue;
+            if (iv[j].a > tc && iv[j].a < te) { te = iv[j].a; je = j; jend = 0; }
+            if (iv[j].b > tc && iv[j].b < te) { te = iv[j].b; je = j; jend = 1; }
+        }
+        if (je < 0) return 0;
+        int before = csg_member(s, o, iv, te, 0), after = csg_member(s, o, iv, te, 1);
+        if (before != after) {
+            int flip = (jend == 0) != (after != 0);
+            ray lr = to_object(r, &s->leaves[o->csg_first + je].w2o);
+            *t = te;
+            *p = v_add(lr.origin, v_scale(lr.dir, te));
+            *face = (je << 4) | (flip << 3) | (jend ? iv[je].fb : iv[je].fa);
+            return 1;
+        }
+        tc = te;
+    }
+}
+
 static int object_intersect(const object *o, ray r, double *t, vec3 *p, int *face) {
     *face = 0;
     switch (o->kind) {
@@ -277,6 +415,7 @@ static int object_intersect(const object *o, ray r, double *t, vec3 *p, int *fac
     case RT_CUBE: return cube_intersect(o, r, t, p, face);
     case RT_CYLINDER: return cylinder_intersect(o, r, t, p, face);
     case RT_CONE: return cone_intersect(o, r, t, p, face);
+    case RT_CSG: return 0; /* needs the scene: closest_hit / in_shadow call csg_intersect */
     }
     return 0;
 }
@@ -293,12 +432,16 @@ static oracle_surface_cb g_surface_cb = NULL;
 static pthread_mutex_t g_cb_lock = PTHREAD_MUTEX_INITIALIZER;
 void oracle_set_surface_callback(oracle_surface_cb cb) { g_surface_cb = cb; }
 
+static int scene_intersect(const scene *s, const object *o, ray r, double *t, vec3 *p, int *face) {
+    return o->kind == RT_CSG ? csg_intersect(s, o, r, t, p, face) : object_intersect(o, r, t, p, face);
+}
+
 static int closest_hit(const scene *s, ray r, hit *h, counters *cnt) {          /* :469-483 */
     int found = 0;
     for (int i = 0; i < s->nobj; i++) {
         double t; vec3 p; int f;
         cnt->tests[s->obj[i].kind]++;
-        if (!object_intersect(&s->obj[i], r, &t, &p, &f)) continue;
+        if (!scene_intersect(s, &s->obj[i], r, &t, &p, &f)) continue;
         if (!found || t < h->t) { found = 1; h->obj = i; h->t = t; h->p = p; h->face = f; }
     }
     return found;
@@ -328,6 +471,12 @@ static void eval_program(int prog, int face, double u, double v, int bad, hitex 
 
 static void surface_props(const scene *s, const hit *h, hitex *x, counters *cnt) {
     const object *o = &s->obj[h->obj];
+    int face = h->face, flip = 0;
+    if (o->kind == RT_CSG) {  /* extension: the leaf that bounds the composite there */
+        flip = (face >> 3) & 1;
+        o = &s->leaves[o->csg_first + (face >> 4)];
+        face &= 7;
+    }
     switch (o->kind) {
     case RT_SPHERE:                                                             /* :106-122 */
         x->pw = m_mulpoint(&o->o2w, h->p);
@@ -339,25 +488,26 @@ static void surface_props(const scene *s, const hit *h, hitex *x, counters *cnt)
         break;
     case RT_CUBE:                                                               /* :242-260 */
         x->pw = m_mulpoint(&o->o2w, h->p);
-        x->nw = o->face[h->face].normal_world;
+        x->nw = o->face[face].normal_world;
         break;
     case RT_CYLINDER: {                                                         /* :339-370 */
         vec3 n;
-        if (h->face == 0) n = V(h->p.x, 0, h->p.z);
-        else if (h->face == 1) n = V(0, 1, 0);
+        if (face == 0) n = V(h->p.x, 0, h->p.z);
+        else if (face == 1) n = V(0, 1, 0);
         else n = V(0, -1, 0);
         x->pw = m_mulpoint(&o->o2w, h->p);
         x->nw = v_norm(m_muldir(&o->normal_mat, n));
         break;
     }
     case RT_CONE: {  /* extension: gradient of x^2 + z^2 - y^2, NormalMat as the cylinder */
-        vec3 n = h->face == 0 ? V(h->p.x, -h->p.y, h->p.z) : V(0, 1, 0);
+        vec3 n = face == 0 ? V(h->p.x, -h->p.y, h->p.z) : V(0, 1, 0);
         x->pw = m_mulpoint(&o->o2w, h->p);
         x->nw = v_norm(m_muldir(&o->normal_mat, n));
         break;
     }
     }
-    int mi = o->material[h->face];
+    if (flip) x->nw = v_neg(x->nw);  /* the composite's outward normal */
+    int mi = o->material[face];
     if (mi >= 0) {
         x->mat = &s->mats[mi];
         return;
@@ -377,7 +527,7 @@ static void surface_props(const scene *s, const hit *h, hitex *x, counters *cnt)
         break;
     case RT_CYLINDER:                                                           /* :339-359 */
     case RT_CONE:  /* extension: the cylinder's coordinates */
-        if (h->face == 0) {
+        if (face == 0) {
             u = (go_atan2(h->p.x, h->p.z) + M_PI) / (2.0 * M_PI);
             v = h->p.y;
         } else {
@@ -386,8 +536,8 @@ static void surface_props(const scene *s, const hit *h, hitex *x, counters *cnt)
         }
         break;
     }
-    int face = (o->kind == RT_PLANE) ? 0 : h->face;
-    eval_program(-mi - 1, face, u, v, bad, x, cnt);
+    int vface = (o->kind == RT_PLANE) ? 0 : face;
+    eval_program(-mi - 1, vface, u, v, bad, x, cnt);
 }
 
 static int in_shadow(const scene *s, const hit *h, const hitex *x, vec3 ldir, double dist, ray r, counters *cnt) { /* :411-429 */
@@ -399,7 +549,7 @@ static int in_shadow(const scene *s, const hit *h, const hitex *x, vec3 ldir, do
         if (i == h->obj) continue;
         double t; vec3 p; int f;
         cnt->shadow_tests[s->obj[i].kind]++;
-        if (!object_intersect(&s->obj[i], sr, &t, &p, &f)) continue;
+        if (!scene_intersect(s, &s->obj[i], sr, &t, &p, &f)) continue;
         if (t * v_len(r.dir) < dist) return 1;
     }
     return 0;
@@ -508,6 +658,39 @@ static vec3 trace_ray(const scene *s, ray r, int depth, counters *cnt) {        
                          col));
 }
 
+static int convert_object(const rt_scene *in, const rt_object *src, object *o) {  /* :756-830 */
+    o->kind = src->kind;
+    if (src->kind < 0 || src->kind >= RT_NUM_KINDS) return RT_E_INVALID;
+    for (int f = 0; f < RT_MAX_FACES; f++) {
+        o->material[f] = src->material[f];
+        if (src->kind != RT_CSG &&
+            (src->material[f] >= in->num_materials || src->material[f] < -in->num_programs)) return RT_E_INVALID;
+    }
+    o->csg_first = src->csg_first;
+    o->csg_count = src->csg_count;
+    o->csg_code = src->csg_code;
+    o->csg_code_len = src->csg_code_len;
+    if (src->has_transform) {                                               /* :757-762 */
+        memcpy(o->o2w.m, src->transform, sizeof(double) * 16);
+        if (!m_inverse(&o->o2w, &o->w2o)) return RT_E_SINGULAR;
+    } else {
+        o->o2w = m_identity();
+        o->w2o = m_identity();
+    }
+    o->normal_mat = m_transpose(&o->w2o);                                   /* :790, :814 */
+    if (o->kind == RT_PLANE) {
+        o->face[0] = create_plane(V(src->plane_point[0], src->plane_point[1], src->plane_point[2]),
+                                  V(src->plane_normal[0], src->plane_normal[1], src->plane_normal[2]), &o->w2o);
+    } else if (o->kind == RT_CUBE) {                                        /* :799-803 */
+        for (int f = 0; f < 6; f++) {
+            o->face[f] = create_plane(V(cube_pts[f][0], cube_pts[f][1], cube_pts[f][2]),
+                                      V(cube_nrm[f][0], cube_nrm[f][1], cube_nrm[f][2]), &o->w2o);
+            o->face[f].side = f;
+        }
+    }
+    return RT_OK;
+}
+
 /* ---- scene conversion (raytracer.go:592-603, 724-830) -------------------- */
 static int convert_scene(const rt_scene *in, scene *s) {
     memset(s, 0, sizeof *s);
@@ -555,38 +738,47 @@ static int convert_scene(const rt_scene *in, scene *s) {
     s->nobj = in->num_objects;
     s->obj = (object *)calloc((size_t)(in->num_objects + 1), sizeof(object));
     for (int i = 0; i < in->num_objects; i++) {
-        const rt_object *src = &in->objects[i];
-        object *o = &s->obj[i];
-        o->kind = src->kind;
-        if (src->kind < 0 || src->kind >= RT_NUM_KINDS) return RT_E_INVALID;
-        for (int f = 0; f < RT_MAX_FACES; f++) {
-            o->material[f] = src->material[f];
-            if (src->material[f] >= in->num_materials || src->material[f] < -in->num_programs) return RT_E_INVALID;
-        }
-        if (src->has_transform) {                                               /* :757-762 */
-            memcpy(o->o2w.m, src->transform, sizeof(double) * 16);
-            if (!m_inverse(&o->o2w, &o->w2o)) return RT_E_SINGULAR;
-        } else {
-            o->o2w = m_identity();
-            o->w2o = m_identity();
-        }
-        o->normal_mat = m_transpose(&o->w2o);                                   /* :790, :814 */
-        if (o->kind == RT_PLANE) {
-            o->face[0] = create_plane(V(src->plane_point[0], src->plane_point[1], src->plane_point[2]),
-                                      V(src->plane_normal[0], src->plane_normal[1], src->plane_normal[2]), &o->w2o);
-        } else if (o->kind == RT_CUBE) {                                        /* :799-803 */
-            for (int f = 0; f < 6; f++) {
-                o->face[f] = create_plane(V(cube_pts[f][0], cube_pts[f][1], cube_pts[f][2]),
-                                          V(cube_nrm[f][0], cube_nrm[f][1], cube_nrm[f][2]), &o->w2o);
-                o->face[f].side = f;
+        int rc = convert_object(in, &in->objects[i], &s->obj[i]);
+        if (rc != RT_OK) return rc;
+    }
+    /* CSG extension: leaves convert like objects; programs are validated */
+    s->nleaves = in->num_csg_leaves > 0 ? in->num_csg_leaves : 0;
+    s->ncode = in->csg_code_words > 0 ? in->csg_code_words : 0;
+    s->code = in->csg_code;
+    s->leaves = (object *)calloc((size_t)(s->nleaves + 1), sizeof(object));
+    for (int i = 0; i < s->nleaves; i++) {
+        int k = in->csg_leaves[i].kind;
+        if (k != RT_SPHERE && k != RT_CUBE && k != RT_CYLINDER && k != RT_PLANE) return RT_E_INVALID;
+        int rc = convert_object(in, &in->csg_leaves[i], &s->leaves[i]);
+        if (rc != RT_OK) return rc;
+    }
+    for (int i = 0; i < s->nobj; i++) {
+        const object *o = &s->obj[i];
+        if (o->kind != RT_CSG) continue;
+        if (o->csg_count <= 0 || o->csg_count > RT_CSG_MAX_LEAVES || o->csg_first < 0 ||
+            o->csg_first + o->csg_count > s->nleaves || o->csg_code < 0 || o->csg_code_len <= 0 ||
+            o->csg_code + o->csg_code_len > s->ncode || !s->code)
+            return RT_E_INVALID;
+        int depth = 0;
+        for (int k = 0; k < o->csg_code_len; k++) {
+            int op = s->code[o->csg_code + k];
+            if (op >= 0) {
+                if (op >= o->csg_count) return RT_E_INVALID;
+                depth++;
+            } else {
+                if (op < RT_CSG_DIFFERENCE || depth < 2) return RT_E_INVALID;
+                depth--;
             }
+            if (depth > RT_CSG_MAX_LEAVES) return RT_E_INVALID;
         }
+        if (depth != 1) return RT_E_INVALID;
     }
     return RT_OK;
 }
 
 static void free_scene(scene *s) {
     free(s->lpos); free(s->lcol); free(s->ldir); free(s->lkind); free(s->lcos); free(s->lexp); free(s->obj);
+    free(s->leaves);
 }
 
 /* ---- Render (raytracer.go:589-682) --------------------------------------- */
@@ -706,7 +898,7 @@ int oracle_intersect(const rt_scene *in, int idx, const double origin[3], const 
     vec3 p = V(0, 0, 0);
     int f = 0;
     double tt = 0;
-    int ok = object_intersect(&s.obj[idx], r, &tt, &p, &f);
+    int ok = scene_intersect(&s, &s.obj[idx], r, &tt, &p, &f);
     if (ok) { *t = tt; point_obj[0] = p.x; point_obj[1] = p.y; point_obj[2] = p.z; *face = f; }
     free_scene(&s);
     return ok;
