@@ -356,6 +356,62 @@ __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r,
   }
 }
 
+__device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(__ballot(b)); }
+
+// Conservative FP32 test: can the segment o + t*d, 0 < t < tmax (d ~ unit)
+// come within the padded bounding sphere (centre c, radius^2 r2)? The exact
+// FP64 test can only report a hit whose point lies inside the object's
+// bounding sphere (to ~1e-12 relative); the host pads the radius by 0.01%
+// plus 1e-4*(1+|c|+|L|) and tmax carries 1e-4 relative slack, ~100x FP32
+// rounding at scene scales, so `false` proves the exact test misses (or, for
+// closestHit, cannot beat the current best).
+struct F3 {
+  float x, y, z;
+};
+__device__ __forceinline__ F3 f3(d3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
+// `slack` (ray_slack) widens the radius by the FP32 rounding scale of the
+// ray origin, so origins far from the object stay conservative.
+__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g, float slack) {
+  const float* b = reinterpret_cast<const float*>(g + 12);
+  float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
+  float tc = ox * d.x + oy * d.y + oz * d.z;
+  tc = fminf(fmaxf(tc, 0.0f), tmax);
+  float qx = ox - tc * d.x, qy = oy - tc * d.y, qz = oz - tc * d.z;
+  const float R = b[3] + slack;
+  return qx * qx + qy * qy + qz * qz <= R * R;
+}
+__device__ __forceinline__ float ray_slack(F3 o) {
+  return 1e-5f * (1.0f + __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z));
+}
+// Conservative FP32 slab test against a BVH node box (built from the padded
+// bounding spheres, rounded outwards), widened by the lane's slack. A
+// component 0 * inf = NaN is ignored by fminf/fmaxf, i.e. a ray parallel to a
+// slab is constrained only by the other axes (it lies on or beyond the
+// widened face otherwise).
+__device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax, const float* nb, float& tn) {
+  const float x0 = (nb[0] - slack - o.x) * id.x, x1 = (nb[3] + slack - o.x) * id.x;
+  const float y0 = (nb[1] - slack - o.y) * id.y, y1 = (nb[4] + slack - o.y) * id.y;
+  const float z0 = (nb[2] - slack - o.z) * id.z, z1 = (nb[5] + slack - o.z) * id.z;
+  tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+  return tn <= tf && tf >= 0.0f && tn <= tmax;
+}
+// Per-wave traversal stack in LDS: node refs and the lanes still active there.
+struct WaveStack {
+  int* ref;
+  uint64_t* mask;
+  __device__ __forceinline__ void push(int& sp, int lane, int r, uint64_t m) {
+    if (lane == 0) {
+      ref[sp] = r;
+      mask[sp] = m;
+    }
+    sp++;
+  }
+};
+__device__ __forceinline__ F3 f3_rcp(F3 d) {
+  return F3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+}
+
 // ---- CSG composites (contest extension; oracle/rt_oracle.c leaf_interval,
 // csg_member, csg_intersect restate the same semantics op for op) ----
 // One convex leaf's interval [a, b] along the ray and the faces it enters /
@@ -462,8 +518,8 @@ __device__ __forceinline__ void leaf_interval(int kind, const double* g, const R
 
 // Postfix membership of the composite just before (after = false) or just
 // after t (bit stacks, depth <= RT_CSG_MAX_LEAVES).
-__device__ __forceinline__ bool csg_member(const int* code, int n, const double* A, const double* B, const int* F,
-                                           double t, bool after) {
+__device__ __forceinline__ bool csg_member(const int* code, int n, const double* A, const double* B, uint64_t live0,
+                                           uint64_t live1, double t, bool after) {
   uint64_t st0 = 0, st1 = 0;
   int sp = 0;
   auto get = [&](int i) -> bool { return ((i < 64 ? st0 >> i : st1 >> (i - 64)) & 1) != 0; };
@@ -476,7 +532,8 @@ __device__ __forceinline__ bool csg_member(const int* code, int n, const double*
   for (int k = 0; k < n; k++) {
     const int op = code[k];
     if (op >= 0) {
-      const bool in = (F[op] & 256) && (after ? (A[op] <= t && t < B[op]) : (A[op] < t && t <= B[op]));
+      const bool live = ((op < 64 ? live0 >> op : live1 >> (op - 64)) & 1) != 0;  // no load for culled leaves
+      const bool in = live && (after ? (A[op] <= t && t < B[op]) : (A[op] < t && t <= B[op]));
       set(sp, in);
       sp++;
     } else {
@@ -491,34 +548,63 @@ __device__ __forceinline__ bool csg_member(const int* code, int n, const double*
 
 // Composite hit: the first leaf end point t > 0 (lowest leaf, entry first,
 // on ties) where membership changes. face = leaf << 4 | flip << 3 | leaf face.
+// Candidates only grow, so the scan stops once te * cut_m reaches cut_lim
+// (strictly beyond, or at-or-beyond when !cut_strict): the caller cannot use
+// such a hit (closest hit: t > best; shadow: t * |d| >= dist), so stopping
+// there changes no result.
 __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, const int* code, int nobj,
-                                        const double* g, const Ray& r, double& t, int& face) {
+                                        const double* g, const Ray& r, double& t, int& face, double cut_m = 1.0,
+                                        double cut_lim = __builtin_inf(), bool cut_strict = true) {
   const int* ci = reinterpret_cast<const int*>(g + 14);
   const int first = nobj + ci[0], count = ci[1];
   const int* prog = code + ci[2];
   const int plen = ci[3];
   double A[RT_CSG_MAX_LEAVES], B[RT_CSG_MAX_LEAVES];
   int F[RT_CSG_MAX_LEAVES];
-  for (int j = 0; j < count; j++) leaf_interval(kinds[first + j], geo + (size_t)(first + j) * GEO, r, A[j], B[j], F[j]);
+  // A leaf whose padded bounding sphere the ray cannot reach for t >= 0 has
+  // an empty interval or one behind the origin: it changes neither the
+  // membership nor the candidates for t > 0, so it is skipped (exact).
+  const F3 of = f3(r.o), df = f3(r.d);
+  const float slack = ray_slack(of);
+  uint64_t live0 = 0, live1 = 0;  // leaves with a non-empty interval, in registers
+  for (int j = 0; j < count; j++) {
+    const int k = kinds[first + j];
+    const double* lg = geo + (size_t)(first + j) * GEO;
+    if (k != RT_PLANE && !may_hit(of, df, 3.0e38f, lg, slack)) continue;
+    leaf_interval(k, lg, r, A[j], B[j], F[j]);
+    if (F[j] & 256) {
+      if (j < 64)
+        live0 |= 1ull << j;
+      else
+        live1 |= 1ull << (j - 64);
+    }
+  }
   double tc = 0.0;
   for (;;) {
     double te = __builtin_inf();
     int je = -1, jend = 0;
-    for (int j = 0; j < count; j++) {
-      if (!(F[j] & 256)) continue;
-      if (A[j] > tc && A[j] < te) {
-        te = A[j];
-        je = j;
-        jend = 0;
-      }
-      if (B[j] > tc && B[j] < te) {
-        te = B[j];
-        je = j;
-        jend = 1;
+    // ascending leaf order over the live set (lowest leaf wins ties)
+    for (int w = 0; w < 2; w++) {
+      uint64_t m = w ? live1 : live0;
+      while (m) {
+        const int j = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        if (A[j] > tc && A[j] < te) {
+          te = A[j];
+          je = j;
+          jend = 0;
+        }
+        if (B[j] > tc && B[j] < te) {
+          te = B[j];
+          je = j;
+          jend = 1;
+        }
       }
     }
     if (je < 0) return false;
-    const bool before = csg_member(prog, plen, A, B, F, te, false), after = csg_member(prog, plen, A, B, F, te, true);
+    if (cut_strict ? te * cut_m > cut_lim : te * cut_m >= cut_lim) return false;
+    const bool before = csg_member(prog, plen, A, B, live0, live1, te, false),
+               after = csg_member(prog, plen, A, B, live0, live1, te, true);
     if (before != after) {
       const int flip = ((jend == 0) != after) ? 1 : 0;
       t = te;
@@ -529,61 +615,6 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
   }
 }
 
-__device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(__ballot(b)); }
-
-// Conservative FP32 test: can the segment o + t*d, 0 < t < tmax (d ~ unit)
-// come within the padded bounding sphere (centre c, radius^2 r2)? The exact
-// FP64 test can only report a hit whose point lies inside the object's
-// bounding sphere (to ~1e-12 relative); the host pads the radius by 0.01%
-// plus 1e-4*(1+|c|+|L|) and tmax carries 1e-4 relative slack, ~100x FP32
-// rounding at scene scales, so `false` proves the exact test misses (or, for
-// closestHit, cannot beat the current best).
-struct F3 {
-  float x, y, z;
-};
-__device__ __forceinline__ F3 f3(d3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
-// `slack` (ray_slack) widens the radius by the FP32 rounding scale of the
-// ray origin, so origins far from the object stay conservative.
-__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g, float slack) {
-  const float* b = reinterpret_cast<const float*>(g + 12);
-  float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
-  float tc = ox * d.x + oy * d.y + oz * d.z;
-  tc = fminf(fmaxf(tc, 0.0f), tmax);
-  float qx = ox - tc * d.x, qy = oy - tc * d.y, qz = oz - tc * d.z;
-  const float R = b[3] + slack;
-  return qx * qx + qy * qy + qz * qz <= R * R;
-}
-__device__ __forceinline__ float ray_slack(F3 o) {
-  return 1e-5f * (1.0f + __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z));
-}
-// Conservative FP32 slab test against a BVH node box (built from the padded
-// bounding spheres, rounded outwards), widened by the lane's slack. A
-// component 0 * inf = NaN is ignored by fminf/fmaxf, i.e. a ray parallel to a
-// slab is constrained only by the other axes (it lies on or beyond the
-// widened face otherwise).
-__device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax, const float* nb, float& tn) {
-  const float x0 = (nb[0] - slack - o.x) * id.x, x1 = (nb[3] + slack - o.x) * id.x;
-  const float y0 = (nb[1] - slack - o.y) * id.y, y1 = (nb[4] + slack - o.y) * id.y;
-  const float z0 = (nb[2] - slack - o.z) * id.z, z1 = (nb[5] + slack - o.z) * id.z;
-  tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-  return tn <= tf && tf >= 0.0f && tn <= tmax;
-}
-// Per-wave traversal stack in LDS: node refs and the lanes still active there.
-struct WaveStack {
-  int* ref;
-  uint64_t* mask;
-  __device__ __forceinline__ void push(int& sp, int lane, int r, uint64_t m) {
-    if (lane == 0) {
-      ref[sp] = r;
-      mask[sp] = m;
-    }
-    sp++;
-  }
-};
-__device__ __forceinline__ F3 f3_rcp(F3 d) {
-  return F3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
-}
 
 // Conservative FP32 test for a plane: can the segment o + t*d, 0 < t < tmax,
 // cross the plane? c = world-space plane (A^T n, n.b + D for WorldToObject
@@ -1056,7 +1087,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           int f;
           bool h;
           if constexpr (CSG)
-            h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, ray, t, f) : object_hit(k, g, ray, t, f);
+            h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, ray, t, f, 1.0,
+                                      found ? best_t : __builtin_inf(), true)
+                            : object_hit(k, g, ray, t, f);
           else
             h = object_hit(k, g, ray, t, f);
           if (h) {
@@ -1275,7 +1308,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             int f;
             bool h;
             if constexpr (CSG)
-              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f) : object_hit(k, g, sr, t, f);
+              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist, false)
+                              : object_hit(k, g, sr, t, f);
             else
               h = object_hit(k, g, sr, t, f);
             if (h) {
@@ -1303,7 +1337,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             int f;
             bool h;
             if constexpr (CSG)
-              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f) : object_hit(k, g, sr, t, f);
+              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist, false)
+                              : object_hit(k, g, sr, t, f);
             else
               h = object_hit(k, g, sr, t, f);
             if (h) {
