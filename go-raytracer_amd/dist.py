@@ -42,9 +42,13 @@ def deinterleave(slabs, height):
     return full[:height]
 
 
+_recv = {}
+
+
 def gather_frame(buf, height, mode="bands", group=None):
     """Gather every rank's buffer to rank 0 and assemble the [H, W, 4] frame
-    there (None elsewhere)."""
+    there (None elsewhere). Rank 0 receives straight into the slices of one
+    reused [world, ...] tensor (no stacking copy)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -52,12 +56,14 @@ def gather_frame(buf, height, mode="bands", group=None):
         return deinterleave(buf.unsqueeze(0), height) if mode == "interleaved" else buf[:height]
     rank = dist.get_rank(group)
     if rank == 0:
-        bufs = [torch.empty_like(buf) for _ in range(world)]
-        dist.gather(buf, gather_list=bufs, dst=0, group=group)
-        stacked = torch.stack(bufs, 0)
+        key = (tuple(buf.shape), buf.dtype, buf.device, world)
+        stacked = _recv.get(key)
+        if stacked is None:
+            stacked = _recv[key] = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+        dist.gather(buf, gather_list=list(stacked.unbind(0)), dst=0, group=group)
         if mode == "interleaved":
             return deinterleave(stacked, height)
-        return stacked.reshape(-1, *buf.shape[1:])[:height]
+        return stacked.reshape(-1, *buf.shape[1:])[:height].clone()  # the receive tensor is reused
     dist.gather(buf, dst=0, group=group)
     return None
 
