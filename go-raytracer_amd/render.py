@@ -31,6 +31,10 @@ def load_library(path=None):
     path = path or os.environ.get("RT_AMD_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RenderError("HIP renderer library not built: %s (run __graft_entry__.build())" % path)
+    # torch bundles its own libamdhip64 (same soname as /opt/rocm's): load it
+    # first so librtamd binds to that one runtime; loading the library first
+    # would put two HIP runtimes in the process and the second finds no device.
+    import torch  # noqa: F401
     l = C.CDLL(path)
     vp, i = C.c_void_p, C.c_int
     l.rt_abi_version.argtypes = []
