@@ -87,7 +87,16 @@ __device__ __forceinline__ double go_min(double x, double y) {
   if (x == 0 && x == y) return signbit64(x) ? x : y;
   return x < y ? x : y;
 }
-__device__ __forceinline__ double clamp01(double x) { return go_min(go_max(x, 0.0), 1.0); }      // vec.go:218
+// The two shapes the path uses, reduced from the rules above with one operand
+// constant: Max(0, v) is v when v > 0 or NaN, else +0 (v = -0 gives +0: the
+// signed-zero rule returns the +0 operand; -Inf gives +0); Min(Max(v, 0), 1)
+// is v in (0, 1), 1 from 1 up to +Inf, +0 at or below 0, NaN for NaN. (A NaN
+// result keeps v's payload where Go returns its canonical NaN; no output of
+// the path depends on a NaN's payload.)
+__device__ __forceinline__ double go_max0(double v) { return (v > 0.0 || v != v) ? v : 0.0; }
+__device__ __forceinline__ double clamp01(double x) {                                         // vec.go:218
+  return x != x ? x : (x > 0.0 ? (x < 1.0 ? x : 1.0) : 0.0);
+}
 __device__ __forceinline__ d3 clamp(d3 c) { return mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)); } // vec.go:110
 
 // math.Modf for f >= 0 (Pow only passes Abs(y)).

@@ -1416,10 +1416,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const double ca = dot(neg(ldir), mk(lt[6], lt[7], lt[8]));
           lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11]) : 0.0);
         }
-        double ndl = go_max(0, dot(nw, ldir));
+        double ndl = go_max0(dot(nw, ldir));
         d3 diffuse = scale(lcol, ndl * M[9]);
         d3 H = norm(add(neg(ray.d), ldir));
-        double spec = go_max(0, dot(nw, H));
+        double spec = go_max0(dot(nw, H));
         d3 specular = scale(lcol, M[10] * go_pow(spec, M[11]));
         L = add(add(L, diffuse), specular);
       }
