@@ -1733,6 +1733,9 @@ struct DevScene {
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0;
 };
 
+#ifndef RT_BVH_SAH
+#define RT_BVH_SAH 1  // binned-SAH splits (median split when degenerate)
+#endif
 // Scenes with at least this many bounded objects use the BVH flavour.
 #ifndef RT_BVH_MIN
 #define RT_BVH_MIN 12
@@ -1805,11 +1808,90 @@ struct BvhBuild {
     int axis = 0;
     for (int k = 1; k < 3; k++)
       if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
-    const int mid = (lo + hi) / 2;
-    std::nth_element(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, [&](int a, int b) {
-      const double ca = (*c)[(size_t)a * 3 + axis], cb = (*c)[(size_t)b * 3 + axis];
-      return ca < cb || (ca == cb && a < b);
-    });
+    int mid = -1;
+#if RT_BVH_SAH
+    // Binned SAH over the centroids (16 bins per axis): minimise
+    // area(left) * n(left) + area(right) * n(right); down to the median split
+    // when every centroid lands in one bin or below depth 40 (keeps the depth,
+    // hence the device stack, bounded).
+    if (depth < 40) {
+      enum { NB = 16 };
+      double best = 1e300;
+      int bax = -1, bbin = -1;
+      for (int ax = 0; ax < 3; ax++) {
+        const double ext = ch[ax] - cl[ax];
+        if (!(ext > 0.0)) continue;
+        double blo[NB][3], bhi[NB][3];
+        int bn[NB] = {0};
+        for (int q = 0; q < NB; q++)
+          for (int k = 0; k < 3; k++) {
+            blo[q][k] = 1e300;
+            bhi[q][k] = -1e300;
+          }
+        for (int j = lo; j < hi; j++) {
+          const int i = ord[j];
+          int q = (int)((((*c)[(size_t)i * 3 + ax]) - cl[ax]) / ext * NB);
+          q = q < 0 ? 0 : (q >= NB ? NB - 1 : q);
+          bn[q]++;
+          for (int k = 0; k < 3; k++) {
+            blo[q][k] = std::min(blo[q][k], (*c)[(size_t)i * 3 + k] - (*r)[i]);
+            bhi[q][k] = std::max(bhi[q][k], (*c)[(size_t)i * 3 + k] + (*r)[i]);
+          }
+        }
+        auto area = [](const double* l, const double* h) {
+          const double dx = h[0] - l[0], dy = h[1] - l[1], dz = h[2] - l[2];
+          return dx < 0 ? 0.0 : dx * dy + dy * dz + dz * dx;
+        };
+        double rl[NB][3], rh[NB][3];
+        int rn[NB];
+        double al[3] = {1e300, 1e300, 1e300}, ah[3] = {-1e300, -1e300, -1e300};
+        int an = 0;
+        for (int q = NB - 1; q >= 0; q--) {
+          for (int k = 0; k < 3; k++) {
+            al[k] = std::min(al[k], blo[q][k]);
+            ah[k] = std::max(ah[k], bhi[q][k]);
+            rl[q][k] = al[k];
+            rh[q][k] = ah[k];
+          }
+          an += bn[q];
+          rn[q] = an;
+        }
+        double ll[3] = {1e300, 1e300, 1e300}, lh[3] = {-1e300, -1e300, -1e300};
+        int ln = 0;
+        for (int q = 0; q < NB - 1; q++) {
+          for (int k = 0; k < 3; k++) {
+            ll[k] = std::min(ll[k], blo[q][k]);
+            lh[k] = std::max(lh[k], bhi[q][k]);
+          }
+          ln += bn[q];
+          if (ln == 0 || rn[q + 1] == 0) continue;
+          const double cost = area(ll, lh) * ln + area(rl[q + 1], rh[q + 1]) * rn[q + 1];
+          if (cost < best) {
+            best = cost;
+            bax = ax;
+            bbin = q;
+          }
+        }
+      }
+      if (bax >= 0) {
+        const double ext = ch[bax] - cl[bax];
+        auto it = std::partition(ord.begin() + lo, ord.begin() + hi, [&](int i) {
+          int q = (int)((((*c)[(size_t)i * 3 + bax]) - cl[bax]) / ext * NB);
+          q = q < 0 ? 0 : (q >= NB ? NB - 1 : q);
+          return q <= bbin;
+        });
+        mid = (int)(it - ord.begin());
+        if (mid <= lo || mid >= hi) mid = -1;
+      }
+    }
+#endif
+    if (mid < 0) {
+      mid = (lo + hi) / 2;
+      std::nth_element(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, [&](int a, int b) {
+        const double ca = (*c)[(size_t)a * 3 + axis], cb = (*c)[(size_t)b * 3 + axis];
+        return ca < cb || (ca == cb && a < b);
+      });
+    }
     const int node = (int)(nodes.size() / BN);
     nodes.resize(nodes.size() + BN, 0.0f);
     const Sub l = build(lo, mid, depth + 1);
