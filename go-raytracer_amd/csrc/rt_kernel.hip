@@ -1385,8 +1385,17 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const bool a0 = act && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb, t0);
             const bool a1 = act && ni[3] < occ && may_hit_box(sof, sidf, sslack, stmax, nb + 6, t1);
             const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+#ifndef RT_SHADOW_NEAR_FIRST
+#define RT_SHADOW_NEAR_FIRST 0
+#endif
+#if RT_SHADOW_NEAR_FIRST
+            // nearer subtree popped first: finds an occluder soonest
+            const bool c1_first = 2 * __popcll(__ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
+#else
             // lower-index subtree popped first: it can prune the other
-            if (ni[3] < ni[2]) {
+            const bool c1_first = ni[3] < ni[2];
+#endif
+            if (c1_first) {
               if (m0) bst.push(ssp, lane, ni[0], m0);
               if (m1) bst.push(ssp, lane, ni[1], m1);
             } else {
