@@ -1386,7 +1386,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const bool a1 = act && ni[3] < occ && may_hit_box(sof, sidf, sslack, stmax, nb + 6, t1);
             const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
 #ifndef RT_SHADOW_NEAR_FIRST
-#define RT_SHADOW_NEAR_FIRST 0
+#define RT_SHADOW_NEAR_FIRST 0  // measured: near-first shadow order is slower (C5 695 -> 822 ms)
 #endif
 #if RT_SHADOW_NEAR_FIRST
             // nearer subtree popped first: finds an occluder soonest
