@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=8)
     p.add_argument("--shard", choices=["interleaved", "bands"], default="interleaved")
+    p.add_argument("--specialize", choices=["on", "off"], default="on",
+                   help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
+                        "before the warmup; bit-identical output)")
     return p.parse_args()
 
 
@@ -103,8 +106,9 @@ def main():
         kw["height"] = args.height
     rargs = cfg(**kw)
     packed = pkg.scene.convert(rargs)
-    ctx = pkg.RenderContext(local)
+    ctx = pkg.RenderContext(local, specialize=args.specialize == "on")
     ctx.set_scene(packed)
+    spec_active, spec_ms = ctx.specialized()
     dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=args.shard)
 
     def barrier():
@@ -172,7 +176,9 @@ def main():
                        "width": packed.width, "height": packed.height, "depth": rargs.depth,
                        "lights": len(rargs.lights), "objects": int(packed.scene.num_objects),
                        "rays_per_frame": int(per_step_rays),
-                       "parallelism": "rows%d-%s" % (world, args.shard)},
+                       "parallelism": "rows%d-%s" % (world, args.shard),
+                       "kernel": "specialised" if spec_active else "generic",
+                       "spec_compile_ms": round(spec_ms, 1)},
             "roofline": {"bound": "valu-fp64", "achieved": round(achieved_tf, 3), "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
                          "frac_nofma_ceiling": round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),

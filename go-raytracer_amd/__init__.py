@@ -13,4 +13,4 @@ Layout:
   gml/                 host GML front end + closure-surface compiler
 """
 from . import abi, configs, dist, gomath, imageio, scene  # noqa: F401
-from .render import Render, RenderContext, load_library  # noqa: F401
+from .render import Render, RenderContext, load_library, spec_precompile  # noqa: F401

@@ -7,7 +7,9 @@
 #pragma once
 #pragma clang fp contract(off)
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 namespace rt {

@@ -1,0 +1,1547 @@
+// rt_render.h -- device side of the render megakernel (see rt_kernel.hip for
+// the execution model and the scene blob layout notes at the top of this file).
+//
+// Compiled twice:
+//   * ahead of time into librtamd.so by rt_kernel.hip (generic flavours:
+//     object count and kinds read from the scene blob at run time);
+//   * at run time through hipRTC when a context enables scene specialisation
+//     (rt_set_specialize): the same source with RT_SPEC_NOBJ / RT_SPEC_KINDS
+//     defined, so the closestHit and inShadow object loops of a small linear
+//     scene are fully unrolled with compile-time primitive kinds. Same
+//     operations in the same order -> bit-identical images and counters.
+#pragma once
+#pragma clang fp contract(off)
+
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#endif
+
+#include "rt_abi.h"
+#include "rt_device.h"
+
+#ifndef RT_SHADE_NUM
+#define RT_SHADE_NUM 3  // shade when >= NUM/DEN of the wave's busy lanes hold a hit
+#endif
+#ifndef RT_SHADE_DEN
+#define RT_SHADE_DEN 4
+#endif
+#ifndef RT_DIV_SKIP
+#define RT_DIV_SKIP 1  // skip divisions whose sign already proves t <= 0 (exact, see t_nonpos)
+#endif
+#ifndef RT_FRAME_PREFETCH
+#define RT_FRAME_PREFETCH 1  // load the parent frame during the TRACE pass
+#endif
+#ifndef RT_CULL
+#define RT_CULL 1  // wave-uniform conservative bounding-sphere culling (exact, see may_hit)
+#endif
+#ifndef RT_LDS_FRAMES
+#define RT_LDS_FRAMES 0  // recursion levels whose frame core lives in LDS (measured: no gain)
+#endif
+#ifndef RT_CUBE_FAST
+#define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
+#endif
+
+using namespace rt;
+
+// ---------------------------------------------------------------------------
+// Scene blob (built by rt_set_scene), one contiguous allocation, 16-B aligned
+// sections; strides in doubles:
+// geo    [nobj][GEO]  0..11 WorldToObject rows 0-2; planes: 12..14 normal, 15 D;
+//                     bounded kinds: 12..13 = 4 floats (centre xyz, padded
+//                     radius^2) of a world-space bounding sphere (culling only)
+// shade  [nobj][SHD]  0..11 ObjectToWorld rows 0-2, 12..29 NormalWorld per face;
+//                     planes: 16..19 = 8 floats of the world-space plane for
+//                     culling (see may_hit_plane)
+// mats   [nmat][MAT]  0..2 colour, 3 reflectivity, 4..5 baked fuzz offset
+//                     (fuzz*cos^2, fuzz*sin^2; raytracer.go:517-521), 6 fuzz>=0,
+//                     7 transparency, 8 ior, 9 kd, 10 ks, 11 specular exponent
+// lights [nl][LGT]    0..2 position, 3..5 colour, 6..8 directional: normalize(-dir),
+//                     spot: normalize(at - pos); 9 kind, 10 spot cos(cutoff),
+//                     11 spot exponent (kinds: include/rt_abi.h RT_LIGHT_*)
+// kind   [nobj] int32;  objmat [nobj][OMAT] int32 per-face material index
+// ---------------------------------------------------------------------------
+enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
+// GLOB record (head of the lights section): 0..2 ambient, 3..5 bg start,
+// 6..8 bg end, 9 viewport width, 10 viewport height (read where used, so they
+// do not occupy scalar registers across the whole kernel)
+// Frame of one traceRay activation that has children (post-order combine).
+// Global layout: 14 fields, lane-interleaved: Lw[3] cfirst[3] pend_o[3]
+// pend_d[3] kr packed. The CORE fields (Lw, kr, packed) of the first
+// RT_LDS_FRAMES levels live in LDS instead; cfirst/pending (only used when a
+// material is both reflective and transparent) always live in HBM.
+enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
+enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
+enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
+       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24 };
+enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
+#ifndef RT_LDS_MAX
+#define RT_LDS_MAX (40 * 1024)
+#endif
+enum { LDS_MAX_BYTES = RT_LDS_MAX };
+
+struct Params {
+  int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
+  int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_csg, off_code, off_consts,
+      off_entry, blob_bytes;
+  int lds_vm_off;     // LDS byte offset of the per-lane VM material records (LDS flavour)
+  double* vm_global;  // per-lane VM material records (global flavour)
+  const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
+  unsigned int* queue;
+  unsigned long long* stats;
+  double* stack;
+  uint32_t* out;
+  int width, height, depth, nobj, nlights, y0, y1, tiles_x;
+  int trow0, trow_stride;  // trow_stride > 0: output tile row j renders image tile row trow0 + j*stride
+  unsigned int total_slots;
+  int frames;  // stack frames per lane (depth - 1, >= 1)
+  // BVH flavour (scenes with many bounded objects)
+  const float* bvh_nodes;  // internal nodes [n][BN] (see BvhBuild)
+  const double* bvh_geo;   // leaf objects in BVH order: geo record, 14 = index, 15 = kind
+  const int* planes;       // unbounded objects, ascending index
+  int nplanes, bvh_stack_off;
+  int cnt_off;    // LDS byte offset of the per-lane event counters [NCNT][WG]
+  int kind_mask;  // bit k: the scene has objects of kind k
+};
+// Per-lane event counters (u64, LDS, fire-and-forget ds_add), reduced once per
+// workgroup at exit: per-wave 64-bit SGPR counters pushed the kernel into
+// SGPR spilling (C2 +33% time, C3 +7%).
+enum { CNT_TRACED = 0, CNT_SHADED = 1, CNT_SURFERR = 2, CNT_ST0 = 3, NCNT = CNT_ST0 + RT_NUM_KINDS };
+enum { PREF = 8 };  // u32 per prefix-count entry (RT_NUM_KINDS used, 16-B aligned)
+// BVH node: child 0 box (lo xyz, hi xyz), child 1 box, then as int: ref 0,
+// ref 1, smallest object index under child 0, under child 1. A ref is
+// (node << 3) for an internal node, (first << 3) | count for a leaf of
+// `count` (1..4) consecutive bvh_geo records.
+enum { BN = 16, BVH_STACK = 64 };
+
+struct Ray {
+  d3 o, d;
+};
+
+// rayToObjectSpace (raytracer.go:51-56) with prim.Mat4.MulPoint/MulDir
+// (vec.go:298-313): m points at the 3x4 affine rows.
+__device__ __forceinline__ Ray to_obj(const double* m, const Ray& r) {
+  Ray l;
+  l.o = mk(m[0] * r.o.x + m[1] * r.o.y + m[2] * r.o.z + m[3], m[4] * r.o.x + m[5] * r.o.y + m[6] * r.o.z + m[7],
+           m[8] * r.o.x + m[9] * r.o.y + m[10] * r.o.z + m[11]);
+  l.d = mk(m[0] * r.d.x + m[1] * r.d.y + m[2] * r.d.z, m[4] * r.d.x + m[5] * r.d.y + m[6] * r.d.z,
+           m[8] * r.d.x + m[9] * r.d.y + m[10] * r.d.z);
+  return l;
+}
+
+// True when q = num/den (den != 0, finite) is certainly <= 0, i.e. num == 0
+// or the signs differ, so the reference would reject t = q (t <= 0) and the
+// division can be skipped. NaN operands return false (the division runs and
+// the NaN flows through exactly as in the reference).
+__device__ __forceinline__ bool t_nonpos(double num, double den) {
+#if RT_DIV_SKIP
+  return (num == 0.0 && !__builtin_isnan(den)) || (num < 0.0 && den > 0.0) || (num > 0.0 && den < 0.0);
+#else
+  return false;
+#endif
+}
+
+// Sphere.Intersect (raytracer.go:58-104): unit sphere, near root only.
+__device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
+  double a = dot(l.d, l.d);
+  double hb = dot(l.o, l.d);
+  double c = dot(l.o, l.o) - 1.0;
+  double disc = hb * hb - a * c;
+  if (disc < 0.0) return false;
+  double sq = __builtin_sqrt(disc);
+  double num = -hb - sq;
+  if (t_nonpos(num, a)) return false;  // t0 <= 0: no near hit
+  double t0 = num / a;
+  if (t0 > 0.0) {
+    t = t0;
+    return true;
+  }
+  return false;
+}
+
+// Plane.Intersect (raytracer.go:164-180) on an object-space ray.
+__device__ __forceinline__ bool plane_hit(const Ray& l, d3 n, double pd, double& t) {
+  double denom = dot(n, l.d);
+  if (__builtin_fabs(denom) < 1e-6) return false;
+  double num = -pd - dot(n, l.o);
+  if (t_nonpos(num, denom)) return false;
+  double tt = num / denom;
+  if (tt <= 0.0) return false;
+  t = tt;
+  return true;
+}
+
+// Cube.Intersect (raytracer.go:214-240) over prim.PlanesForUnitCube
+// (internal/prim/plane.go:29-38). Every face re-transforms the ray with the
+// same matrix in the reference, so one transform gives identical values.
+// With RT_CUBE_FAST the face planes' dot products are evaluated on the one
+// non-zero axis: for a finite ray, n.v = (0*a + 0*b) + (+-1)*c equals +-c
+// exactly whenever c != 0, and when c == 0 both forms are a zero that is
+// rejected identically (|denom| < 1e-6, or t = 0 <= 0), so hits, T and
+// PointObj are bit-identical to the generic dot products.
+__device__ __forceinline__ bool cube_face(const Ray& l, int f, double& best, int& bf, bool& found) {
+  // face f: axis, sign of the normal, -D (D = -normal.Dot(point))
+  const int ax = (f < 2) ? 2 : ((f < 4) ? 0 : 1);
+  const bool pos = (f == 1 || f == 3 || f == 4);
+  const double negD = (f == 1 || f == 3 || f == 4) ? 1.0 : 0.0;
+  double dA = ax == 0 ? l.d.x : (ax == 1 ? l.d.y : l.d.z);
+  double oA = ax == 0 ? l.o.x : (ax == 1 ? l.o.y : l.o.z);
+  double denom = pos ? dA : -dA;
+  if (__builtin_fabs(denom) < 1e-6) return false;
+  double nO = pos ? oA : -oA;
+  double num = negD - nO;
+  if (t_nonpos(num, denom)) return false;
+  double tt = num / denom;
+  if (tt <= 0.0) return false;
+  d3 p = add(l.o, scale(l.d, tt));
+  if (p.x < 0 || p.x > 1 || p.y < 0 || p.y > 1 || p.z < 0 || p.z > 1) return false;
+  if (!found || tt < best) {
+    found = true;
+    best = tt;
+    bf = f;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool cube_hit(const Ray& l, double& t, int& face) {
+  bool found = false;
+  double best = 0.0;
+  int bf = 0;
+#if RT_CUBE_FAST
+#pragma unroll
+  for (int f = 0; f < 6; f++) cube_face(l, f, best, bf, found);
+#else
+  const double N[6][3] = {{0, 0, -1}, {0, 0, 1}, {-1, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, -1, 0}};
+  const double D[6] = {-0.0, -1.0, -0.0, -1.0, -1.0, -0.0};
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    double ft;
+    if (!plane_hit(l, mk(N[f][0], N[f][1], N[f][2]), D[f], ft)) continue;
+    if (ft < 0.0) continue;
+    d3 p = add(l.o, scale(l.d, ft));
+    if (p.x < 0 || p.x > 1 || p.y < 0 || p.y > 1 || p.z < 0 || p.z > 1) continue;
+    if (!found || ft < best) {
+      found = true;
+      best = ft;
+      bf = f;
+    }
+  }
+#endif
+  if (found) {
+    t = best;
+    face = bf;
+  }
+  return found;
+}
+
+// Cylinder.Intersect (raytracer.go:279-337).
+// Cylinder.Intersect (raytracer.go:279-337) and, with cone = true, the
+// contest-extension cone (oracle/rt_oracle.c cone_intersect; not in the
+// reference): the same quadric-plus-caps structure, so one routine (the flag
+// is wave-uniform) keeps register pressure at the cylinder's. Every quantity
+// is formed in the oracle's op order: the cone's a, halfB, c0 append
+// "- dy*dy", "- oy*dy", "- oy*oy" where the cylinder has nothing / "- 1.0".
+__device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, bool cone) {
+  double bestT = __builtin_inf();
+  int bestFace = -1;
+  double a = l.d.x * l.d.x + l.d.z * l.d.z;
+  double hb = l.o.x * l.d.x + l.o.z * l.d.z;
+  double c0 = l.o.x * l.o.x + l.o.z * l.o.z;
+  if (cone) {
+    a = a - l.d.y * l.d.y;
+    hb = hb - l.o.y * l.d.y;
+    c0 = c0 - l.o.y * l.o.y;
+  } else {
+    c0 = c0 - 1.0;
+  }
+  if (__builtin_fabs(a) > 1e-12) {  // cylinder: a >= 0, the reference's a > 1e-12
+    double disc = hb * hb - a * c0;
+    if (disc >= 0.0) {
+      double sq = __builtin_sqrt(disc);
+      // consider() ignores t <= 0 (raytracer.go:287), so a root whose sign is
+      // known to be non-positive needs no division.
+      double n0 = -hb - sq, n1 = -hb + sq;
+      if (!t_nonpos(n0, a)) {
+        double t0 = n0 / a;
+        double y0 = l.o.y + l.d.y * t0;
+        if (y0 >= 0.0 && y0 <= 1.0 && t0 > 0.0 && t0 < bestT) {
+          bestT = t0;
+          bestFace = 0;
+        }
+      }
+      if (!t_nonpos(n1, a)) {
+        double t1 = n1 / a;
+        double y1 = l.o.y + l.d.y * t1;
+        if (y1 >= 0.0 && y1 <= 1.0 && t1 > 0.0 && t1 < bestT) {
+          bestT = t1;
+          bestFace = 0;
+        }
+      }
+    }
+  } else if (cone && __builtin_fabs(hb) > 1e-12) {  // cone: ray parallel to a generator
+    double n0 = -c0, den = 2.0 * hb;
+    if (!t_nonpos(n0, den)) {
+      double t0 = n0 / den;
+      double y0 = l.o.y + l.d.y * t0;
+      if (y0 >= 0.0 && y0 <= 1.0 && t0 > 0.0 && t0 < bestT) {
+        bestT = t0;
+        bestFace = 0;
+      }
+    }
+  }
+  if (__builtin_fabs(l.d.y) > 1e-12) {
+    double nTop = 1.0 - l.o.y;
+    if (!t_nonpos(nTop, l.d.y)) {
+      double tTop = nTop / l.d.y;
+      double px = l.o.x + l.d.x * tTop, pz = l.o.z + l.d.z * tTop;
+      if (px * px + pz * pz <= 1.0 && tTop > 0.0 && tTop < bestT) {
+        bestT = tTop;
+        bestFace = 1;
+      }
+    }
+    double nBot = -l.o.y;
+    if (!cone && !t_nonpos(nBot, l.d.y)) {
+      double tBot = nBot / l.d.y;
+      double px = l.o.x + l.d.x * tBot, pz = l.o.z + l.d.z * tBot;
+      if (px * px + pz * pz <= 1.0 && tBot > 0.0 && tBot < bestT) {
+        bestT = tBot;
+        bestFace = 2;
+      }
+    }
+  }
+  if (bestFace < 0) return false;
+  t = bestT;
+  face = bestFace;
+  return true;
+}
+
+
+// One SceneObject.Intersect on a world-space ray; k is wave-uniform.
+__device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r, double& t, int& face) {
+  Ray l = to_obj(g, r);
+  face = 0;
+  switch (k) {
+    case RT_SPHERE:
+      return sphere_hit(l, t);
+    case RT_PLANE:
+      return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
+    case RT_CUBE:
+      return cube_hit(l, t, face);
+    default:  // RT_CYLINDER, RT_CONE
+      return quadric_hit(l, t, face, k == RT_CONE);
+  }
+}
+
+__device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(__ballot(b)); }
+
+// Conservative FP32 test: can the segment o + t*d, 0 < t < tmax (d ~ unit)
+// come within the padded bounding sphere (centre c, radius^2 r2)? The exact
+// FP64 test can only report a hit whose point lies inside the object's
+// bounding sphere (to ~1e-12 relative); the host pads the radius by 0.01%
+// plus 1e-4*(1+|c|+|L|) and tmax carries 1e-4 relative slack, ~100x FP32
+// rounding at scene scales, so `false` proves the exact test misses (or, for
+// closestHit, cannot beat the current best).
+struct F3 {
+  float x, y, z;
+};
+__device__ __forceinline__ F3 f3(d3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
+// `slack` (ray_slack) widens the radius by the FP32 rounding scale of the
+// ray origin, so origins far from the object stay conservative.
+__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g, float slack) {
+  const float* b = reinterpret_cast<const float*>(g + 12);
+  float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
+  float tc = ox * d.x + oy * d.y + oz * d.z;
+  tc = fminf(fmaxf(tc, 0.0f), tmax);
+  float qx = ox - tc * d.x, qy = oy - tc * d.y, qz = oz - tc * d.z;
+  const float R = b[3] + slack;
+  return qx * qx + qy * qy + qz * qz <= R * R;
+}
+__device__ __forceinline__ float ray_slack(F3 o) {
+  return 1e-5f * (1.0f + __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z));
+}
+// Conservative FP32 slab test against a BVH node box (built from the padded
+// bounding spheres, rounded outwards), widened by the lane's slack. A
+// component 0 * inf = NaN is ignored by fminf/fmaxf, i.e. a ray parallel to a
+// slab is constrained only by the other axes (it lies on or beyond the
+// widened face otherwise).
+__device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax, const float* nb, float& tn) {
+  const float x0 = (nb[0] - slack - o.x) * id.x, x1 = (nb[3] + slack - o.x) * id.x;
+  const float y0 = (nb[1] - slack - o.y) * id.y, y1 = (nb[4] + slack - o.y) * id.y;
+  const float z0 = (nb[2] - slack - o.z) * id.z, z1 = (nb[5] + slack - o.z) * id.z;
+  tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+  return tn <= tf && tf >= 0.0f && tn <= tmax;
+}
+// Per-wave traversal stack in LDS: node refs and the lanes still active there.
+struct WaveStack {
+  int* ref;
+  uint64_t* mask;
+  __device__ __forceinline__ void push(int& sp, int lane, int r, uint64_t m) {
+    if (lane == 0) {
+      ref[sp] = r;
+      mask[sp] = m;
+    }
+    sp++;
+  }
+};
+__device__ __forceinline__ F3 f3_rcp(F3 d) {
+  return F3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+}
+
+// ---- CSG composites (contest extension; oracle/rt_oracle.c leaf_interval,
+// csg_member, csg_intersect restate the same semantics op for op) ----
+// One convex leaf's interval [a, b] along the ray and the faces it enters /
+// leaves by: f = fa | fb << 4 | 256 when non-empty.
+__device__ __forceinline__ void leaf_interval(int kind, const double* g, const Ray& r, double& a, double& b, int& f) {
+  const Ray l = to_obj(g, r);
+  a = -__builtin_inf();
+  b = __builtin_inf();
+  int fa = 0, fb = 0;
+  bool ok = true;
+  if (kind == RT_SPHERE) {
+    const double qa = dot(l.d, l.d), hb = dot(l.o, l.d), c = dot(l.o, l.o) - 1.0;
+    const double disc = hb * hb - qa * c;
+    if (disc < 0.0) {
+      ok = false;
+    } else {
+      const double sq = __builtin_sqrt(disc);
+      a = (-hb - sq) / qa;
+      b = (-hb + sq) / qa;
+    }
+  } else if (kind == RT_CUBE) {
+    const double o3[3] = {l.o.x, l.o.y, l.o.z}, d3v[3] = {l.d.x, l.d.y, l.d.z};
+    const int flo[3] = {2, 5, 0}, fhi[3] = {3, 4, 1};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (d3v[k] == 0.0) {
+        if (o3[k] < 0.0 || o3[k] > 1.0) ok = false;
+        continue;
+      }
+      const double ta = (0.0 - o3[k]) / d3v[k], tb = (1.0 - o3[k]) / d3v[k];
+      double lo = ta, hi = tb;
+      int fl = flo[k], fh = fhi[k];
+      if (d3v[k] < 0.0) {
+        lo = tb;
+        hi = ta;
+        fl = fhi[k];
+        fh = flo[k];
+      }
+      if (lo > a) {
+        a = lo;
+        fa = fl;
+      }
+      if (hi < b) {
+        b = hi;
+        fb = fh;
+      }
+    }
+    if (a > b) ok = false;
+  } else if (kind == RT_CYLINDER) {
+    const double qa = l.d.x * l.d.x + l.d.z * l.d.z;
+    if (qa > 1e-12) {
+      const double hb = l.o.x * l.d.x + l.o.z * l.d.z;
+      const double c0 = l.o.x * l.o.x + l.o.z * l.o.z - 1.0;
+      const double disc = hb * hb - qa * c0;
+      if (disc < 0.0) {
+        ok = false;
+      } else {
+        const double sq = __builtin_sqrt(disc);
+        a = (-hb - sq) / qa;
+        b = (-hb + sq) / qa;
+      }
+    } else if (l.o.x * l.o.x + l.o.z * l.o.z > 1.0) {
+      ok = false;
+    }
+    if (ok) {
+      if (__builtin_fabs(l.d.y) > 1e-12) {
+        const double tb0 = (0.0 - l.o.y) / l.d.y, tt = (1.0 - l.o.y) / l.d.y;
+        double lo = tb0, hi = tt;
+        int fl = 2, fh = 1;
+        if (l.d.y < 0.0) {
+          lo = tt;
+          hi = tb0;
+          fl = 1;
+          fh = 2;
+        }
+        if (lo > a) {
+          a = lo;
+          fa = fl;
+        }
+        if (hi < b) {
+          b = hi;
+          fb = fh;
+        }
+      } else if (l.o.y < 0.0 || l.o.y > 1.0) {
+        ok = false;
+      }
+      if (a > b) ok = false;
+    }
+  } else {  // RT_PLANE: the half-space n.p + D <= 0
+    const d3 n = mk(g[12], g[13], g[14]);
+    const double denom = dot(n, l.d);
+    if (__builtin_fabs(denom) < 1e-6) {
+      if (dot(n, l.o) + g[15] > 0.0) ok = false;
+    } else {
+      const double tt = (-g[15] - dot(n, l.o)) / denom;
+      if (denom < 0.0)
+        a = tt;
+      else
+        b = tt;
+    }
+  }
+  f = fa | (fb << 4) | (ok ? 256 : 0);
+}
+
+// Postfix membership of the composite just before (after = false) or just
+// after t (bit stacks, depth <= RT_CSG_MAX_LEAVES).
+__device__ __forceinline__ bool csg_member(const int* code, int n, const double* A, const double* B, uint64_t live0,
+                                           uint64_t live1, double t, bool after) {
+  uint64_t st0 = 0, st1 = 0;
+  int sp = 0;
+  auto get = [&](int i) -> bool { return ((i < 64 ? st0 >> i : st1 >> (i - 64)) & 1) != 0; };
+  auto set = [&](int i, bool v) {
+    if (i < 64)
+      st0 = v ? (st0 | (1ull << i)) : (st0 & ~(1ull << i));
+    else
+      st1 = v ? (st1 | (1ull << (i - 64))) : (st1 & ~(1ull << (i - 64)));
+  };
+  for (int k = 0; k < n; k++) {
+    const int op = code[k];
+    if (op >= 0) {
+      const bool live = ((op < 64 ? live0 >> op : live1 >> (op - 64)) & 1) != 0;  // no load for culled leaves
+      const bool in = live && (after ? (A[op] <= t && t < B[op]) : (A[op] < t && t <= B[op]));
+      set(sp, in);
+      sp++;
+    } else {
+      sp -= 2;
+      const bool x = get(sp), y = get(sp + 1);
+      set(sp, op == RT_CSG_UNION ? (x || y) : (op == RT_CSG_INTERSECT ? (x && y) : (x && !y)));
+      sp++;
+    }
+  }
+  return (st0 & 1) != 0;
+}
+
+// Composite hit: the first leaf end point t > 0 (lowest leaf, entry first,
+// on ties) where membership changes. face = leaf << 4 | flip << 3 | leaf face.
+// Candidates only grow, so the scan stops once te * cut_m reaches cut_lim
+// (strictly beyond, or at-or-beyond when !cut_strict): the caller cannot use
+// such a hit (closest hit: t > best; shadow: t * |d| >= dist), so stopping
+// there changes no result.
+__device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, const int* code, int nobj,
+                                        const double* g, const Ray& r, double& t, int& face, double cut_m = 1.0,
+                                        double cut_lim = __builtin_inf(), bool cut_strict = true) {
+  const int* ci = reinterpret_cast<const int*>(g + 14);
+  const int first = nobj + ci[0], count = ci[1];
+  const int* prog = code + ci[2];
+  const int plen = ci[3];
+  double A[RT_CSG_MAX_LEAVES], B[RT_CSG_MAX_LEAVES];
+  int F[RT_CSG_MAX_LEAVES];
+  // A leaf whose padded bounding sphere the ray cannot reach for t >= 0 has
+  // an empty interval or one behind the origin: it changes neither the
+  // membership nor the candidates for t > 0, so it is skipped (exact).
+  const F3 of = f3(r.o), df = f3(r.d);
+  const float slack = ray_slack(of);
+  uint64_t live0 = 0, live1 = 0;  // leaves with a non-empty interval, in registers
+  for (int j = 0; j < count; j++) {
+    const int k = kinds[first + j];
+    const double* lg = geo + (size_t)(first + j) * GEO;
+    if (k != RT_PLANE && !may_hit(of, df, 3.0e38f, lg, slack)) continue;
+    leaf_interval(k, lg, r, A[j], B[j], F[j]);
+    if (F[j] & 256) {
+      if (j < 64)
+        live0 |= 1ull << j;
+      else
+        live1 |= 1ull << (j - 64);
+    }
+  }
+  double tc = 0.0;
+  for (;;) {
+    double te = __builtin_inf();
+    int je = -1, jend = 0;
+    // ascending leaf order over the live set (lowest leaf wins ties)
+    for (int w = 0; w < 2; w++) {
+      uint64_t m = w ? live1 : live0;
+      while (m) {
+        const int j = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        if (A[j] > tc && A[j] < te) {
+          te = A[j];
+          je = j;
+          jend = 0;
+        }
+        if (B[j] > tc && B[j] < te) {
+          te = B[j];
+          je = j;
+          jend = 1;
+        }
+      }
+    }
+    if (je < 0) return false;
+    if (cut_strict ? te * cut_m > cut_lim : te * cut_m >= cut_lim) return false;
+    const bool before = csg_member(prog, plen, A, B, live0, live1, te, false),
+               after = csg_member(prog, plen, A, B, live0, live1, te, true);
+    if (before != after) {
+      const int flip = ((jend == 0) != after) ? 1 : 0;
+      t = te;
+      face = (je << 4) | (flip << 3) | (jend ? (F[je] >> 4) & 15 : F[je] & 15);
+      return true;
+    }
+    tc = te;
+  }
+}
+
+
+// Conservative FP32 test for a plane: can the segment o + t*d, 0 < t < tmax,
+// cross the plane? c = world-space plane (A^T n, n.b + D for WorldToObject
+// p -> A p + b) followed by its term-magnitude scale (sum_r |n_r||a_rc|,
+// sum_r |n_r||b_r| + |D|). The reference decides a hit from the signs of
+// f(0) = n.o_obj + D and f(tmax) (t = -f(0)/denom compared with tmax), each
+// computed in FP64 with error ~1e-15 of that scale; here both are evaluated
+// in FP32 and `false` needs them to agree in sign with a 1e-4 margin, so the
+// exact test misses (or cannot beat the current best). tmax >= 1e30 means no
+// bound: then f(0) and the slope must agree in sign (the root lies behind).
+__device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, const double* sh) {
+  const float* c = reinterpret_cast<const float*>(sh + 16);
+  const float f0 = c[0] * o.x + c[1] * o.y + c[2] * o.z + c[3];
+  const float sl = c[0] * d.x + c[1] * d.y + c[2] * d.z;
+  const float a0 = c[4] * __builtin_fabsf(o.x) + c[5] * __builtin_fabsf(o.y) + c[6] * __builtin_fabsf(o.z) + c[7];
+  const float a1 = c[4] * __builtin_fabsf(d.x) + c[5] * __builtin_fabsf(d.y) + c[6] * __builtin_fabsf(d.z);
+  float f1, m0, m1;
+  if (tmax >= 1e30f) {
+    f1 = sl;
+    m0 = 1e-4f * a0 + 1e-30f;
+    m1 = 1e-4f * a1 + 1e-30f;
+  } else {
+    f1 = f0 + tmax * sl;
+    m0 = 1e-4f * (a0 + tmax * a1) + 1e-30f;
+    m1 = m0;
+  }
+  return !((f0 > m0 && f1 > m1) || (f0 < -m0 && f1 < -m1));
+}
+
+// Diagnostic build only (-DRT_PHASE_TIMING): wave cycles per phase, stamped
+// with s_memtime into per-wave scalar sums; never enabled in the product.
+#ifdef RT_PHASE_TIMING
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PH_BEGIN() uint64_t ph_t0_ = stamp()
+#define PH_MARK(k)              \
+  do {                          \
+    uint64_t t_ = stamp();      \
+    ph_acc[k] += t_ - ph_t0_;   \
+    ph_t0_ = t_;                \
+  } while (0)
+#else
+#define PH_BEGIN() (void)0
+#define PH_MARK(k) (void)0
+#endif
+
+// Frame stack: lane-interleaved so that one field of one frame is a
+// contiguous 512-B row for the wave.
+__device__ __forceinline__ double* frame_ptr(double* base, int frame) { return base + (size_t)frame * FRAME_FIELDS * 64; }
+__device__ __forceinline__ void st3(double* f, int field, d3 v) {
+  f[(field + 0) * 64] = v.x;
+  f[(field + 1) * 64] = v.y;
+  f[(field + 2) * 64] = v.z;
+}
+__device__ __forceinline__ d3 ld3(const double* f, int field) {
+  return mk(f[(field + 0) * 64], f[(field + 1) * 64], f[(field + 2) * 64]);
+}
+
+// CORE field c (0..2 Lw, 3 kr, 4 packed) -> global field index.
+__device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ? 12 : 13); }
+
+// Frame flags (packed with the material index).
+enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16 };
+
+// ---------------------------------------------------------------------------
+// Closure-surface VM: executes a straight-line register
+// program compiled on the host from a GML surface function
+// (go-raytracer_amd/gml/surface_compiler.py) -- the device counterpart of
+// EvalSurfaceFn (evaluator.go:672-727). Registers are 64-bit (f64 / i64 /
+// bool); r0..r9 = Material, r10 = face, r11 = u, r12 = v. Go semantics:
+// int64 wraparound, truncating divi/modi, floor/frac via amd64 float->int,
+// Cephes sin/cos on degrees * (Pi/180). Returns true on a run-time error
+// (the reference would panic).
+// ---------------------------------------------------------------------------
+enum VmOp {
+  VM_NOP, VM_CONST, VM_MOV, VM_ADDF, VM_SUBF, VM_MULF, VM_DIVF, VM_NEGF, VM_ADDI, VM_SUBI, VM_MULI, VM_DIVI,
+  VM_MODI, VM_NEGI, VM_LTF, VM_EQF, VM_LTI, VM_EQI, VM_SEL, VM_FLOOR, VM_FRAC, VM_SQRT, VM_SIN, VM_COS,
+  VM_CLAMPF, VM_CLAMPI, VM_TBL, VM_AND, VM_OR, VM_NOT, VM_ERR, VM_RET
+};
+enum { VM_REGS = 64, VM_MAX_STEPS = 8192 };
+
+// Inlined: as an out-of-line call reading the LDS-staged program through
+// generic pointers it rendered wrong pixels on gfx950 (measured: the global
+// blob path and the inlined call are exact), and inlining needs less scratch.
+__device__ __forceinline__ bool run_vm(const uint32_t* code, const uint64_t* consts, int pc, long long face, double u,
+                                    double v, double* out) {
+  uint64_t R[VM_REGS];
+  R[10] = (uint64_t)face;
+  R[11] = (uint64_t)__double_as_longlong(u);
+  R[12] = (uint64_t)__double_as_longlong(v);
+  bool err = false;
+#define F_(r) __longlong_as_double((long long)R[r])
+#define I_(r) ((long long)R[r])
+#define SETF(x) R[d] = (uint64_t)__double_as_longlong(x)
+  for (int steps = 0; steps < VM_MAX_STEPS; steps++, pc += 2) {
+    const uint32_t w0 = code[pc], c = code[pc + 1];
+    const int op = (int)(w0 & 0xff), d = (int)((w0 >> 8) & 0x3f), a = (int)((w0 >> 16) & 0x3f),
+              b = (int)((w0 >> 24) & 0x3f);
+    switch (op) {
+      case VM_RET:
+        for (int k = 0; k < 10; k++) out[k] = F_(k);
+        return err;
+      case VM_CONST: R[d] = consts[c]; break;
+      case VM_MOV: R[d] = R[a]; break;
+      case VM_ADDF: SETF(F_(a) + F_(b)); break;
+      case VM_SUBF: SETF(F_(a) - F_(b)); break;
+      case VM_MULF: SETF(F_(a) * F_(b)); break;
+      case VM_DIVF: SETF(F_(a) / F_(b)); break;
+      case VM_NEGF: SETF(-F_(a)); break;
+      case VM_ADDI: R[d] = R[a] + R[b]; break;
+      case VM_SUBI: R[d] = R[a] - R[b]; break;
+      case VM_MULI: R[d] = R[a] * R[b]; break;
+      case VM_DIVI: {  // Go: truncating; MinInt64 / -1 wraps; /0 is checked by ERR
+        long long x = I_(a), y = I_(b);
+        R[d] = y == 0 ? 0 : (y == -1 ? (uint64_t)0 - (uint64_t)x : (uint64_t)(x / y));
+        break;
+      }
+      case VM_MODI: {
+        long long x = I_(a), y = I_(b);
+        R[d] = (y == 0 || y == -1) ? 0 : (uint64_t)(x % y);
+        break;
+      }
+      case VM_NEGI: R[d] = (uint64_t)0 - R[a]; break;
+      case VM_LTF: R[d] = F_(a) < F_(b); break;
+      case VM_EQF: R[d] = F_(a) == F_(b); break;
+      case VM_LTI: R[d] = I_(a) < I_(b); break;
+      case VM_EQI: R[d] = R[a] == R[b]; break;
+      case VM_SEL: R[d] = R[a] ? R[b] : R[c & 0x3f]; break;
+      case VM_FLOOR: {
+        double x = F_(a);
+        R[d] = (uint64_t)go_f2i(__builtin_isfinite(x) ? __builtin_floor(x) : x);
+        break;
+      }
+      case VM_FRAC: {
+        double x = F_(a);
+        SETF(x - (double)go_f2i(x));
+        break;
+      }
+      case VM_SQRT: SETF(__builtin_sqrt(F_(a))); break;
+      case VM_SIN: SETF(go_sin(0.017453292519943295 * F_(a))); break;
+      case VM_COS: SETF(go_cos(0.017453292519943295 * F_(a))); break;
+      case VM_CLAMPF: {
+        double x = F_(a);
+        SETF(x < 0 ? 0.0 : (x > 1 ? 1.0 : x));
+        break;
+      }
+      case VM_CLAMPI: {
+        long long x = I_(a);
+        R[d] = (uint64_t)(x < 0 ? 0 : (x > 1 ? 1 : x));
+        break;
+      }
+      case VM_TBL: {  // consts[c] = n, then n entries; bounds are checked by ERR
+        long long n = (long long)consts[c], i = I_(a);
+        i = i < 0 ? 0 : (i >= n ? n - 1 : i);
+        R[d] = consts[c + 1 + i];
+        break;
+      }
+      case VM_AND: R[d] = (R[a] != 0) && (R[b] != 0); break;
+      case VM_OR: R[d] = (R[a] != 0) || (R[b] != 0); break;
+      case VM_NOT: R[d] = R[a] == 0; break;
+      case VM_ERR: err = err || (R[a] != 0); break;
+      default: return true;
+    }
+  }
+#undef F_
+#undef I_
+#undef SETF
+  return true;  // malformed program (no RET)
+}
+
+// traceRay's final combine (raytracer.go:557-561).
+__device__ __forceinline__ d3 combine(bool tmode, d3 lw, d3 col, double refl, double kr, d3 R, d3 Tr) {
+  if (!tmode) return clamp(mul(add(lw, scale(R, refl)), col));
+  return clamp(mul(add(lw, add(scale(R, kr), scale(Tr, 1.0 - kr))), col));
+}
+
+struct View {
+  const int* entry;
+  const uint32_t* code;
+  const uint64_t* consts;
+  const double* geo;
+  const double* shade;
+  const double* mats;
+  const double* lights;
+  const int* kind;
+  const int* objmat;
+  const uint32_t* pref;  // [nobj + 1][PREF]: objects of each kind with index < i
+  const int* csg;        // CSG postfix programs (extension)
+};
+
+template <bool LDS, bool BVH, bool CSG>
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 3  // 168 VGPRs -> 3 waves/SIMD (C3 on par with 4; C2 -10%, C4 (BVH) -4%)
+#endif
+__global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char* __restrict__ blob, Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const char* base;
+  if constexpr (LDS) {
+    // Stage the whole scene once per workgroup (the only block-wide barrier).
+    const int n16 = P.blob_bytes / 16;
+    for (int i = threadIdx.x; i < n16; i += WG)
+      reinterpret_cast<uint4*>(smem)[i] = reinterpret_cast<const uint4*>(blob)[i];
+    __syncthreads();
+    base = smem;
+  } else {
+    base = blob;
+  }
+  View S;
+  S.geo = reinterpret_cast<const double*>(base + P.off_geo);
+  S.shade = reinterpret_cast<const double*>(base + P.off_shade);
+  S.mats = reinterpret_cast<const double*>(base + P.off_mats);
+  // lights section: a 16-double record of per-frame constants, then the lights
+  const double* G = reinterpret_cast<const double*>(base + P.off_lights);
+  S.lights = G + GLOB;
+  S.kind = reinterpret_cast<const int*>(base + P.off_kind);
+  S.objmat = reinterpret_cast<const int*>(base + P.off_objmat);
+  S.pref = reinterpret_cast<const uint32_t*>(base + P.off_pref);
+  S.csg = reinterpret_cast<const int*>(base + P.off_csg);
+  S.code = reinterpret_cast<const uint32_t*>(base + P.off_code);
+  S.entry = reinterpret_cast<const int*>(base + P.off_entry);
+  S.consts = reinterpret_cast<const uint64_t*>(base + P.off_consts);
+
+  const int lane = (int)(threadIdx.x & 63);
+  const int wslot = (int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
+  double* stk = P.stack + (size_t)wslot * ((size_t)P.frames * FRAME_FIELDS * 64) + lane;
+  double* lfr = reinterpret_cast<double*>(smem + P.lds_frames_off) +
+                (size_t)(threadIdx.x >> 6) * (RT_LDS_FRAMES * CORE * 64) + lane;
+  // frame core accessors: level < RT_LDS_FRAMES in LDS, deeper in HBM
+  auto core_ld = [&](int level, int c) -> double {
+    if (level < RT_LDS_FRAMES) return lfr[(level * CORE + c) * 64];
+    return frame_ptr(stk, level)[core_gfield(c) * 64];
+  };
+  auto core_st = [&](int level, int c, double v) {
+    if (level < RT_LDS_FRAMES)
+      lfr[(level * CORE + c) * 64] = v;
+    else
+      frame_ptr(stk, level)[core_gfield(c) * 64] = v;
+  };
+  // Per-lane material record written by the surface VM (same layout as mats).
+  double* vmrec;
+  if constexpr (LDS)
+    vmrec = reinterpret_cast<double*>(smem + P.lds_vm_off) + (size_t)threadIdx.x * MAT;
+  else
+    vmrec = P.vm_global + ((size_t)wslot * 64 + lane) * MAT;
+  const d3 eye = mk(0.0, 0.0, -1.0);  // raytracer.go:605-609
+
+  // lane state
+  int state = S_IDLE;
+  bool need_gen = false;  // lane waits for its next sample ray
+  int px = 0, py = 0, sample = 0, sp = 0;
+  unsigned int pout = 0;  // output pixel index
+  int hit_i = 0, hit_f = 0;
+  double hit_t = 0.0;
+  Pcg rng{0, 0};
+  d3 sum = mk(0, 0, 0);
+  Ray ray;
+  ray.o = mk(0, 0, 0);
+  ray.d = mk(0, 0, 1);
+
+  // wave-uniform pool and counters
+  unsigned int pool_next = 0, pool_end = 0;
+  bool exhausted = false;
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off);
+  for (int k = 0; k < NCNT; k++) cnt[k * WG + threadIdx.x] = 0;
+  auto cnt_add = [&](int k, uint64_t v) { atomicAdd(&cnt[k * WG + threadIdx.x], (unsigned long long)v); };
+  WaveStack bst;
+  bst.mask = reinterpret_cast<uint64_t*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
+  bst.ref = reinterpret_cast<int*>(smem + P.bvh_stack_off + WAVES_PER_WG * BVH_STACK * 8) + (threadIdx.x >> 6) * BVH_STACK;
+#ifdef RT_PHASE_TIMING
+  uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t bd_tnodes = 0, bd_snodes = 0, bd_tleaf = 0, bd_sleaf = 0, bd_trays = 0, bd_srays = 0;
+#ifdef RT_COST_MAP
+  uint32_t lane_cost = 0;  // node visits charged to this lane's pixel (diagnostic)
+#endif
+#endif
+
+  const double W1 = (double)(P.width - 1), H1 = (double)(P.height - 1);
+
+  // New sample ray: raytracer.go:642-649.
+  auto gen_ray = [&]() {
+    double dx = pcg_float64(rng) - 0.5;
+    double dy = pcg_float64(rng) - 0.5;
+    const double vw = G[9], vh = G[10];
+    double u = ((double)px + dx) / W1 * vw - vw / 2.0;
+    double v = ((double)py + dy) / H1 * vh - vh / 2.0;
+    ray.o = mk(u, -v, 0.0);
+    ray.d = norm(sub(ray.o, eye));
+  };
+
+  // Propagate a finished traceRay colour up the lane's frame stack
+  // (post-order, raytracer.go:528/554/557-561); ends with the lane either
+  // tracing its next ray (pending refraction child / next sample) or idle.
+  auto unwind = [&](bool have_res, d3 res, bool pf_valid, long long pf_packed, d3 pf_lw, double pf_kr) {
+    while (__any(have_res)) {
+      if (have_res) {
+        if (sp == 0) {
+          sum = add(sum, res);  // raytracer.go:651
+          sample++;
+          if (sample == 4) {
+            d3 c = scale(sum, 1.0 / 4.0);  // raytracer.go:656 -> vec.go:104-107
+            uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
+            uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
+            uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
+#ifdef RT_COST_MAP
+            P.out[pout] = lane_cost;
+            lane_cost = 0;
+#else
+            P.out[pout] =
+                (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+#endif
+            state = S_IDLE;
+          } else {
+            need_gen = true;  // next sample ray, generated in one uniform block
+            state = S_TRACE;
+          }
+          have_res = false;
+        } else {
+          double* f = frame_ptr(stk, sp - 1);
+          long long packed;
+          if (pf_valid)
+            packed = pf_packed;
+          else
+            packed = __double_as_longlong(core_ld(sp - 1, 4));
+          int fl = (int)(packed & 0xff);
+          if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
+            // reflection child done; trace the pending refraction child
+            st3(f, 3, res);
+            core_st(sp - 1, 4, __longlong_as_double(packed | FL_STAGE));
+            ray.o = ld3(f, 6);
+            ray.d = ld3(f, 9);
+            state = S_TRACE;
+            have_res = false;
+          } else {
+            const double* FM = S.mats + (size_t)(packed >> 8) * MAT;
+            d3 R = mk(0, 0, 0), Tr = mk(0, 0, 0);
+            if ((fl & FL_HASR) && (fl & FL_HAST)) {
+              R = ld3(f, 3);
+              Tr = res;
+            } else if (fl & FL_HASR) {
+              R = res;
+            } else {
+              Tr = res;
+            }
+            d3 lw;
+            double kr;
+            if (pf_valid) {
+              lw = pf_lw;
+              kr = pf_kr;
+            } else {
+              lw = mk(core_ld(sp - 1, 0), core_ld(sp - 1, 1), core_ld(sp - 1, 2));
+              kr = core_ld(sp - 1, 3);
+            }
+            d3 fcol;
+            double frefl;
+            if (fl & FL_VMMAT) {
+              fcol = ld3(f, 14);
+              frefl = f[17 * 64];
+            } else {
+              fcol = mk(FM[0], FM[1], FM[2]);
+              frefl = FM[3];
+            }
+            res = combine((fl & FL_TMODE) != 0, lw, fcol, frefl, kr, R, Tr);
+            sp--;
+          }
+          pf_valid = false;
+        }
+      }
+    }
+  };
+
+  PH_BEGIN();
+  for (;;) {
+    // ---- refill idle lanes from the wave pool (one 8x8 tile per chunk) ----
+    for (;;) {
+      bool need = state == S_IDLE;
+      uint64_t mask = __ballot(need);
+      if (mask == 0 || exhausted) break;
+      if (pool_next >= pool_end) {
+        unsigned int b = 0;
+        if (lane == 0) b = atomicAdd(P.queue, (unsigned int)CHUNK);
+        b = __shfl(b, 0);
+        if (b >= P.total_slots) {
+          exhausted = true;
+          break;
+        }
+        pool_next = b;
+        pool_end = min(b + (unsigned int)CHUNK, P.total_slots);
+      }
+      unsigned int rank = __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
+      unsigned int take = min((unsigned int)__popcll(mask), pool_end - pool_next);
+      if (need && rank < take) {
+        unsigned int slot = pool_next + rank;
+        unsigned int tile = slot / (TILE * TILE), within = slot % (TILE * TILE);
+        const int trow = (int)(tile / (unsigned)P.tiles_x);
+        const int x = (int)((tile % (unsigned)P.tiles_x) * TILE + within % TILE);
+        const int orow = trow * TILE + (int)(within / TILE);
+        const int y = P.trow_stride > 0 ? (P.trow0 + trow * P.trow_stride) * TILE + (int)(within / TILE) : P.y0 + orow;
+        if (x < P.width && y < P.y1) {
+          px = x;
+          py = y;
+          pout = (unsigned int)orow * (unsigned int)P.width + (unsigned int)x;
+          // rng = PCG(0xDEAD^x, 0xBEEF^ymin) advanced 8*(y%20) draws
+          // (raytracer.go:632-643: 2 draws per sample, 4 samples per row).
+          int ymin = y - y % 20;
+          Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
+          const uint64_t* j = P.jump + (size_t)(y % 20) * 4;
+          rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
+          sample = 0;
+          sum = mk(0, 0, 0);
+          sp = 0;
+          need_gen = true;
+          state = S_TRACE;
+        }
+      }
+      pool_next += take;
+    }
+    if (!__any(state != S_IDLE)) break;
+    // ---- new sample rays for every lane that needs one, in one block ----
+    if (__any(need_gen)) {
+      if (need_gen) {
+        gen_ray();
+        need_gen = false;
+      }
+    }
+    PH_MARK(0);
+
+    // ---- TRACE pass: closestHit over all objects (raytracer.go:469-483) ----
+    if (__any(state == S_TRACE)) {
+      const bool tr = state == S_TRACE;
+      // Prefetch the parent frame: a ray that misses pops it right after
+      // this pass, and the load latency hides under the object loop.
+      bool pf = false;
+      long long pf_packed = 0;
+      d3 pf_lw = mk(0, 0, 0);
+      double pf_kr = 0.0;
+#if RT_FRAME_PREFETCH
+      if (tr && sp > 0) {
+        pf = true;
+        pf_packed = __double_as_longlong(core_ld(sp - 1, 4));
+        pf_lw = mk(core_ld(sp - 1, 0), core_ld(sp - 1, 1), core_ld(sp - 1, 2));
+        pf_kr = core_ld(sp - 1, 3);
+      }
+#endif
+      bool found = false;
+      double best_t = 0.0;
+      int best_i = 0, best_f = 0;
+      const F3 of = f3(ray.o), df = f3(ray.d);
+      const float slack = ray_slack(of);
+      // One closestHit candidate (object i, wave-uniform) for the lanes in `act`.
+      // The linear loop visits objects in index order (strict <, the first
+      // index wins ties); the BVH visits them in any order and breaks ties on
+      // the index explicitly, which selects the same object.
+      auto trace_obj = [&](int i, int k, const double* g, bool act) {
+        bool test = act;
+#if RT_CULL
+        // an object entered beyond the lane's current best cannot win (strict <)
+        const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+        test = test && (k != RT_PLANE ? may_hit(of, df, tmax, g, slack)
+                                      : may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
+        if (!__any(test)) return;
+#endif
+        if (test) {
+          double t;
+          int f;
+          bool h;
+          if constexpr (CSG)
+            h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, ray, t, f, 1.0,
+                                      found ? best_t : __builtin_inf(), true)
+                            : object_hit(k, g, ray, t, f);
+          else
+            h = object_hit(k, g, ray, t, f);
+          if (h) {
+            if (!found || t < best_t || (BVH && t == best_t && i < best_i)) {
+              found = true;
+              best_t = t;
+              best_i = i;
+              best_f = f;
+            }
+          }
+        }
+      };
+      if constexpr (!BVH) {
+#ifdef RT_SPEC_NOBJ
+        {
+          constexpr int spec_k[RT_SPEC_NOBJ] = {RT_SPEC_KINDS};
+#pragma unroll
+          for (int i = 0; i < RT_SPEC_NOBJ; i++) trace_obj(i, spec_k[i], S.geo + (size_t)i * GEO, tr);
+        }
+#else
+        for (int i = 0; i < P.nobj; i++) trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
+#endif
+      } else {
+        for (int p = 0; p < P.nplanes; p++) {  // unbounded objects: planes, unbounded CSG
+          const int i = P.planes[p];
+          trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
+        }
+        const F3 idf = f3_rcp(df);
+#ifdef RT_PHASE_TIMING
+        bd_trays++;
+#endif
+        int ssp = 0;
+        bst.push(ssp, lane, 0, __ballot(tr));
+        while (ssp > 0) {
+          ssp--;
+          const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
+          const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+          const bool act = tr && ((m >> lane) & 1);
+#ifdef RT_PHASE_TIMING
+          bd_tnodes++;
+#ifdef RT_COST_MAP
+          if (tr) lane_cost++;
+#endif
+#endif
+          if (r & 7) {  // leaf
+#ifdef RT_PHASE_TIMING
+            bd_tleaf++;
+#endif
+            const int first = r >> 3, count = r & 7;
+            for (int j = first; j < first + count; j++) {
+              const double* g = P.bvh_geo + (size_t)j * GEO;
+              const int* gi = reinterpret_cast<const int*>(g + 14);
+              trace_obj(gi[0], gi[2], g, act);
+            }
+          } else {
+            const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
+            const int* ni = reinterpret_cast<const int*>(nb + 12);
+            const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+            float t0, t1;
+            const bool a0 = act && may_hit_box(of, idf, slack, tmax, nb, t0);
+            const bool a1 = act && may_hit_box(of, idf, slack, tmax, nb + 6, t1);
+            const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+            // near child popped first: the one most lanes enter first
+            const bool c1_first = 2 * __popcll(__ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
+            if (c1_first) {
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+            } else {
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+            }
+          }
+        }
+      }
+      if (tr) cnt_add(CNT_TRACED, 1);
+      PH_MARK(1);
+      d3 res = mk(0, 0, 0);
+      if (tr) {
+        if (found) {
+          state = S_SHADE;
+          hit_i = best_i;
+          hit_f = best_f;
+          hit_t = best_t;
+        } else {  // background gradient, raytracer.go:493-497
+          double t = 0.5 * (ray.d.y + 1.0);
+          res = lerp(mk(G[3], G[4], G[5]), mk(G[6], G[7], G[8]), t);
+        }
+      }
+      unwind(tr && !found, res, pf, pf_packed, pf_lw, pf_kr);
+      PH_MARK(2);
+    }
+
+    // ---- SHADE pass, once enough lanes hold a hit ----
+    const uint64_t nsh = popc_ballot(state == S_SHADE);
+    const uint64_t ntr = popc_ballot(state == S_TRACE);
+    if (nsh == 0 || (ntr != 0 && nsh * RT_SHADE_DEN < (nsh + ntr) * RT_SHADE_NUM)) continue;
+
+    const bool hit = state == S_SHADE;
+    if (hit) cnt_add(CNT_SHADED, 1);
+    // ComputeSurfaceProps (raytracer.go:106-122, 182-194, 242-260, 339-370)
+    d3 pw = mk(0, 0, 0), nw = mk(0, 0, 1);
+    int mat = 0;
+    bool surf_bad = false;
+    if (hit) {
+      int si = hit_i, sf = hit_f;  // the surface: the object, or a CSG composite's leaf
+      bool flip = false;
+      if constexpr (CSG) {
+        if (S.kind[hit_i] == RT_CSG) {
+          const int* ci = reinterpret_cast<const int*>(S.geo + (size_t)hit_i * GEO + 14);
+          si = P.nobj + ci[0] + (hit_f >> 4);
+          flip = ((hit_f >> 3) & 1) != 0;
+          sf = hit_f & 7;
+        }
+      }
+      const double* g = S.geo + (size_t)si * GEO;
+      const double* s = S.shade + (size_t)si * SHD;
+      const int k = S.kind[si];
+      Ray l = to_obj(g, ray);
+      d3 p = add(l.o, scale(l.d, hit_t));  // Hit.PointObj
+      pw = mk(s[0] * p.x + s[1] * p.y + s[2] * p.z + s[3], s[4] * p.x + s[5] * p.y + s[6] * p.z + s[7],
+              s[8] * p.x + s[9] * p.y + s[10] * p.z + s[11]);
+      if (k == RT_SPHERE) {
+        nw = p;
+      } else if (k == RT_CYLINDER || k == RT_CONE) {
+        d3 n = sf == 0 ? (k == RT_CONE ? mk(p.x, -p.y, p.z) : mk(p.x, 0, p.z)) : (sf == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
+        // NormalMat = WorldToObject^T (raytracer.go:814): MulDir then Normalize.
+        nw = norm(mk(g[0] * n.x + g[4] * n.y + g[8] * n.z, g[1] * n.x + g[5] * n.y + g[9] * n.z,
+                     g[2] * n.x + g[6] * n.y + g[10] * n.z));
+      } else {
+        nw = mk(s[12 + sf * 3], s[13 + sf * 3], s[14 + sf * 3]);
+      }
+      if (flip) nw = neg(nw);  // the composite's outward normal
+      mat = S.objmat[(size_t)si * OMAT + sf];
+      if (mat < 0) {
+        // Closure surface: (face, u, v) as ComputeSurfaceProps computes them
+        // (raytracer.go:124-150, 196-205, 249, 339-359), then the VM.
+        double u, v;
+        bool bad = false;
+        long long face = (k == RT_PLANE) ? 0 : sf;
+        if (k == RT_SPHERE) {
+          bad = __builtin_fabs(p.y) > 1;
+          v = (p.y + 1.0) / 2.0;
+          u = go_acos(p.z / __builtin_sqrt(1.0 - p.y * p.y)) / 6.283185307179586;
+        } else if ((k == RT_CYLINDER || k == RT_CONE) && sf == 0) {
+          u = (go_atan2(p.x, p.z) + 3.141592653589793) / 6.283185307179586;
+          v = p.y;
+        } else {
+          u = p.x;
+          v = p.z;
+        }
+        double r[10];
+        bad = run_vm(S.code, S.consts, S.entry[-mat - 1], face, u, v, r) || bad;
+        if (bad)  // counted; the material reads as all-zero (oracle convention)
+          for (int k = 0; k < 10; k++) r[k] = 0.0;
+        vmrec[0] = r[0];
+        vmrec[1] = r[1];
+        vmrec[2] = r[2];
+        vmrec[3] = r[3];
+        const double fz = r[4];
+        if (fz >= 0) {  // baked constant fuzz offset (raytracer.go:516-522)
+          const double cf = go_cos(fz), sf = go_sin(fz);
+          vmrec[4] = fz * cf * cf;
+          vmrec[5] = fz * sf * sf;
+          vmrec[6] = 1.0;
+        } else {
+          vmrec[4] = vmrec[5] = vmrec[6] = 0.0;
+        }
+        vmrec[7] = r[5];
+        vmrec[8] = r[6];
+        vmrec[9] = r[7];
+        vmrec[10] = r[8];
+        vmrec[11] = r[9];
+        surf_bad = bad;
+      }
+    }
+    if (surf_bad) cnt_add(CNT_SURFERR, 1);
+
+    // computeLighting + inShadow (raytracer.go:372-429)
+    PH_MARK(3);
+    const double* M = mat >= 0 ? S.mats + (size_t)mat * MAT : vmrec;
+    d3 L = mk(0, 0, 0);
+    if (hit) L = scale(mk(G[0], G[1], G[2]), M[9]);
+    const double rlen = len(ray.d);
+    const d3 sorig = add(pw, scale(nw, 1e-4));
+    uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind (cones: below)
+    for (int li = 0; li < P.nlights; li++) {
+      const double* lt = S.lights + (size_t)li * LGT;
+      const int lkind = (int)lt[9];  // wave-uniform
+      d3 ldir;
+      double dist;
+      if (lkind == RT_LIGHT_DIRECTIONAL) {  // extension: light at infinity
+        ldir = mk(lt[6], lt[7], lt[8]);
+        dist = __builtin_inf();
+      } else {
+        d3 lth = sub(mk(lt[0], lt[1], lt[2]), pw);
+        dist = len(lth);
+        ldir = norm(lth);
+      }
+      bool open = hit;  // lanes still looking for an occluder
+      Ray sr;
+      sr.o = sorig;
+      sr.d = ldir;
+      const F3 sof = f3(sorig), sdf = f3(ldir);
+      const float sslack = ray_slack(sof);
+      // occluders must lie within t < dist / |ray.d| (raytracer.go:424)
+      const float stmax = (float)(dist / rlen) * 1.0001f + 1e-4f;
+      // inShadow's test count is #{i < end, i != hit} with end = first
+      // occluder + 1 (or nobj); counted per kind from the prefix table below.
+      int send = P.nobj;
+      if constexpr (!BVH) {
+#ifdef RT_SPEC_NOBJ
+        constexpr int spec_k2[RT_SPEC_NOBJ] = {RT_SPEC_KINDS};
+#pragma unroll
+        for (int i = 0; i < RT_SPEC_NOBJ; i++) {
+          if (!__any(open)) break;
+          const int k = spec_k2[i];
+#else
+        for (int i = 0; i < P.nobj; i++) {
+          if (!__any(open)) break;
+          const int k = S.kind[i];
+#endif
+          const double* g = S.geo + (size_t)i * GEO;
+          bool test = open && i != hit_i;
+#if RT_CULL
+          test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
+                                        : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!__any(test)) continue;
+#endif
+          if (test) {
+            double t;
+            int f;
+            bool h;
+            if constexpr (CSG)
+              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist, false)
+                              : object_hit(k, g, sr, t, f);
+            else
+              h = object_hit(k, g, sr, t, f);
+            if (h) {
+              if (t * rlen < dist) {
+                open = false;
+                send = i + 1;
+              }
+            }
+          }
+        }
+      } else {
+        // The reference stops at the first occluder in index order and its
+        // test count is #{i <= that index, i != hit}; the BVH finds the
+        // lowest-index occluder (pruning subtrees whose smallest index is not
+        // lower than the best so far) and derives the count from prefix
+        // counts per kind. The shadow verdict is the same either way.
+        int occ = 0x7fffffff;
+        auto shadow_obj = [&](int i, int k, const double* g, bool act) {
+          bool test = act && i != hit_i && i < occ;
+          test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
+                                        : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!__any(test)) return;
+          if (test) {
+            double t;
+            int f;
+            bool h;
+            if constexpr (CSG)
+              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist, false)
+                              : object_hit(k, g, sr, t, f);
+            else
+              h = object_hit(k, g, sr, t, f);
+            if (h) {
+              if (t * rlen < dist) occ = i;
+            }
+          }
+        };
+        for (int p = 0; p < P.nplanes; p++) {
+          const int i = P.planes[p];
+          shadow_obj(i, S.kind[i], S.geo + (size_t)i * GEO, hit);
+        }
+        const F3 sidf = f3_rcp(sdf);
+#ifdef RT_PHASE_TIMING
+        bd_srays++;
+#endif
+        int ssp = 0;
+        bst.push(ssp, lane, 0, __ballot(hit));
+        while (ssp > 0) {
+          ssp--;
+          const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
+          const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+          const bool act = hit && ((m >> lane) & 1);
+#ifdef RT_PHASE_TIMING
+          bd_snodes++;
+#ifdef RT_COST_MAP
+          if (hit) lane_cost++;
+#endif
+#endif
+          if (r & 7) {  // leaf
+#ifdef RT_PHASE_TIMING
+            bd_sleaf++;
+#endif
+            const int first = r >> 3, count = r & 7;
+            for (int j = first; j < first + count; j++) {
+              const double* g = P.bvh_geo + (size_t)j * GEO;
+              const int* gi = reinterpret_cast<const int*>(g + 14);
+              shadow_obj(gi[0], gi[2], g, act);
+            }
+          } else {
+            const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
+            const int* ni = reinterpret_cast<const int*>(nb + 12);
+            float t0, t1;
+            const bool a0 = act && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb, t0);
+            const bool a1 = act && ni[3] < occ && may_hit_box(sof, sidf, sslack, stmax, nb + 6, t1);
+            const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+#ifndef RT_SHADOW_NEAR_FIRST
+#define RT_SHADOW_NEAR_FIRST 0  // measured: near-first shadow order is slower (C5 695 -> 822 ms)
+#endif
+#if RT_SHADOW_NEAR_FIRST
+            // nearer subtree popped first: finds an occluder soonest
+            const bool c1_first = 2 * __popcll(__ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
+#else
+            // lower-index subtree popped first: it can prune the other
+            const bool c1_first = ni[3] < ni[2];
+#endif
+            if (c1_first) {
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+            } else {
+              if (m1) bst.push(ssp, lane, ni[1], m1);
+              if (m0) bst.push(ssp, lane, ni[0], m0);
+            }
+          }
+        }
+        open = hit && occ == 0x7fffffff;
+        send = open ? P.nobj : occ + 1;
+      }
+      if (hit) {
+        const uint4 pe = *reinterpret_cast<const uint4*>(S.pref + (size_t)send * PREF);
+        const uint32_t pe4 = S.pref[(size_t)send * PREF + 4];
+        const int hk = hit_i < send ? S.kind[hit_i] : -1;
+        sc0 += pe.x - (hk == 0 ? 1u : 0u);
+        sc1 += pe.y - (hk == 1 ? 1u : 0u);
+        sc2 += pe.z - (hk == 2 ? 1u : 0u);
+        sc3 += pe.w - (hk == 3 ? 1u : 0u);
+        if (P.kind_mask & 16) cnt_add(CNT_ST0 + 4, pe4 - (hk == 4 ? 1u : 0u));  // cones, CSG: rare, flushed per light
+        if (P.kind_mask & 32) cnt_add(CNT_ST0 + 5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
+      }
+      PH_MARK(4);
+      if (hit && open) {
+        d3 lcol = mk(lt[3], lt[4], lt[5]);
+        if (lkind == RT_LIGHT_SPOT) {  // extension: cone falloff
+          const double ca = dot(neg(ldir), mk(lt[6], lt[7], lt[8]));
+          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11]) : 0.0);
+        }
+        double ndl = go_max0(dot(nw, ldir));
+        d3 diffuse = scale(lcol, ndl * M[9]);
+        d3 H = norm(add(neg(ray.d), ldir));
+        double spec = go_max0(dot(nw, H));
+        d3 specular = scale(lcol, M[10] * go_pow(spec, M[11]));
+        L = add(add(L, diffuse), specular);
+      }
+      PH_MARK(5);
+    }
+    if (hit) {
+      if (P.kind_mask & 1) cnt_add(CNT_ST0 + 0, sc0);
+      if (P.kind_mask & 2) cnt_add(CNT_ST0 + 1, sc1);
+      if (P.kind_mask & 4) cnt_add(CNT_ST0 + 2, sc2);
+      if (P.kind_mask & 8) cnt_add(CNT_ST0 + 3, sc3);
+    }
+
+    // traceRay body after lighting (raytracer.go:505-561)
+    bool have_res = false;
+    d3 res = mk(0, 0, 0);
+    if (hit) {
+      d3 col = mk(M[0], M[1], M[2]);
+      double refl = M[3], T = M[7];
+      if (refl == 0 && T == 0) {
+        res = clamp(mul(L, col));
+        have_res = true;
+      } else {
+        bool hasR = refl > 0;
+        Ray rr;
+        rr.o = mk(0, 0, 0);
+        rr.d = mk(0, 0, 1);
+        if (hasR) {
+          d3 rd = sub(ray.d, scale(nw, 2.0 * dot(ray.d, nw)));
+          if (M[6] != 0.0) rd = add(rd, mk(M[4], M[5], 0.0));
+          rr.o = add(pw, scale(nw, 1e-4));
+          rr.d = norm(rd);
+        }
+        bool tmode = T > 0;
+        bool hasT = false;
+        Ray trr;
+        trr.o = mk(0, 0, 0);
+        trr.d = mk(0, 0, 1);
+        double kr = 0.0;
+        d3 lw = L;
+        if (tmode) {
+          double n1 = 1.0, n2 = M[8];
+          d3 nn = nw;
+          if (dot(ray.d, nn) > 0.0) {
+            n1 = M[8];
+            n2 = 1.0;
+            nn = scale(nn, -1.0);
+          }
+          // refract (raytracer.go:438-450)
+          double ratio = n1 / n2;
+          double cosI = -dot(nn, ray.d);
+          double sinT2 = ratio * ratio * (1.0 - cosI * cosI);
+          if (!(sinT2 > 1.0)) {
+            double cosT = __builtin_sqrt(1.0 - sinT2);
+            d3 td = add(scale(ray.d, ratio), scale(nn, ratio * cosI - cosT));
+            if (!iszero(td)) {
+              hasT = true;
+              trr.o = sub(pw, scale(nn, 1e-4));
+              trr.d = td;
+            }
+          }
+          // fresnel (raytracer.go:456-467) on the unflipped normal
+          double cosi = dot(ray.d, nw) / (len(ray.d) * len(nw));
+          double r0 = (1.0 - M[8]) / (1.0 + M[8]);
+          r0 = r0 * r0;
+          double cost = __builtin_fabs(cosi);
+          kr = r0 + (1 - r0) * go_pow(1 - cost, 5);
+          lw = scale(L, 1.0 - T);
+        }
+        const int d = P.depth - sp;  // depth of the current ray
+        if (d - 1 > 0 && (hasR || hasT)) {
+          core_st(sp, 0, lw.x);
+          core_st(sp, 1, lw.y);
+          core_st(sp, 2, lw.z);
+          if (hasR && hasT) {
+            double* f = frame_ptr(stk, sp);
+            st3(f, 6, trr.o);
+            st3(f, 9, trr.d);
+          }
+          core_st(sp, 3, kr);
+          if (mat < 0) {  // the VM record is per lane: keep what the combine needs
+            double* f = frame_ptr(stk, sp);
+            st3(f, 14, col);
+            f[17 * 64] = refl;
+          }
+          long long packed = ((long long)(mat < 0 ? 0 : mat) << 8) | (mat < 0 ? FL_VMMAT : 0) |
+                             (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
+          core_st(sp, 4, __longlong_as_double(packed));
+          sp++;
+          ray = hasR ? rr : trr;
+          state = S_TRACE;
+        } else {
+          res = combine(tmode, lw, col, refl, kr, mk(0, 0, 0), mk(0, 0, 0));
+          have_res = true;
+        }
+      }
+    }
+    PH_MARK(6);
+    unwind(have_res, res, false, 0, mk(0, 0, 0), 0.0);
+    PH_MARK(7);
+  }
+
+  if (lane == 0) {
+#ifdef RT_PHASE_TIMING
+    for (int k = 0; k < N_PHASE; k++) atomicAdd(P.stats + ST_PHASE + k, (unsigned long long)ph_acc[k]);
+    atomicAdd(P.stats + ST_BVHDIAG + 0, (unsigned long long)bd_tnodes);
+    atomicAdd(P.stats + ST_BVHDIAG + 1, (unsigned long long)bd_snodes);
+    atomicAdd(P.stats + ST_BVHDIAG + 2, (unsigned long long)bd_tleaf);
+    atomicAdd(P.stats + ST_BVHDIAG + 3, (unsigned long long)bd_sleaf);
+    atomicAdd(P.stats + ST_BVHDIAG + 4, (unsigned long long)bd_trays);
+    atomicAdd(P.stats + ST_BVHDIAG + 5, (unsigned long long)bd_srays);
+#endif
+  }
+  // Workgroup reduction of the per-lane counters (every wave of the group
+  // leaves the main loop, so all reach the barrier).
+  __syncthreads();
+  if (threadIdx.x < NCNT) {
+    unsigned long long sum = 0;
+    for (int j = 0; j < WG; j++) sum += cnt[threadIdx.x * WG + j];
+    const int k = (int)threadIdx.x;
+    const int slot = k == CNT_TRACED ? ST_TRACED : (k == CNT_SHADED ? ST_SHADED : (k == CNT_SURFERR ? ST_SURFERR : ST_STESTS + (k - CNT_ST0)));
+    if (sum) atomicAdd(P.stats + slot, sum);
+    // one inShadow call per (shaded hit, light)
+    if (k == CNT_SHADED && sum) atomicAdd(P.stats + ST_SHADOW, sum * (unsigned long long)P.nlights);
+  }
+}

@@ -59,6 +59,12 @@ def load_library(path=None):
     l.rt_debug_run_surface.restype = i
     l.rt_ssim_rgba8.argtypes = [vp, vp, vp, i, i, C.POINTER(C.c_double), vp]
     l.rt_ssim_rgba8.restype = i
+    l.rt_set_specialize.argtypes = [vp, i]
+    l.rt_set_specialize.restype = i
+    l.rt_specialized.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
+    l.rt_specialized.restype = i
+    l.rt_spec_precompile.argtypes = [i, C.POINTER(i), C.POINTER(C.c_double)]
+    l.rt_spec_precompile.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
     l.rt_render.restype = i
     if l.rt_abi_version() != abi.RT_ABI_VERSION:
@@ -82,7 +88,7 @@ def _packed(scene_or_args):
 class RenderContext:
     """One device context: scene resident in HBM, renders rows on a torch stream."""
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, specialize=False):
         import torch
         if not torch.cuda.is_available():
             raise RenderError("no HIP device visible: the renderer has no CPU path")
@@ -94,6 +100,8 @@ class RenderContext:
             _check(self.lib.rt_create(self.device, C.byref(h)), "rt_create")
         self.handle = h
         self.packed = None
+        if specialize:
+            self.set_specialize(True)
 
     def close(self):
         if self.handle:
@@ -110,6 +118,19 @@ class RenderContext:
         self.packed = _packed(scene_or_args)
         _check(self.lib.rt_set_scene(self.handle, self.packed.ref()), "rt_set_scene")
         return self.packed
+
+    def set_specialize(self, enable=True):
+        """Render small linear scenes (<= 8 objects) with a kernel compiled for
+        their object kinds (hipRTC, ~1-2 s once per scene shape and process;
+        bit-identical output). Raises RenderError if hipRTC fails."""
+        _check(self.lib.rt_set_specialize(self.handle, int(bool(enable))), "rt_set_specialize")
+
+    def specialized(self):
+        """(active, compile_ms): whether the current scene runs a specialised
+        kernel and what preparing it cost (0 on a cache hit)."""
+        a, ms = C.c_int(), C.c_double()
+        _check(self.lib.rt_specialized(self.handle, C.byref(a), C.byref(ms)), "rt_specialized")
+        return bool(a.value), ms.value
 
     def render_rows_async(self, y0, y1, out, stream=None):
         """Enqueue rows [y0, y1) into the uint8 CUDA tensor `out` ([y1-y0, W, 4])."""
@@ -192,6 +213,17 @@ class RenderContext:
         self.render_rows_async(y0, y1, out)
         torch.cuda.synchronize(self.device)
         return out.cpu().numpy()
+
+
+def spec_precompile(kinds):
+    """Compile (no device needed) the specialised kernel for a scene whose
+    objects have these primitive kinds, in order; returns the compile time (ms,
+    0 if already cached in this process)."""
+    lib = load_library()
+    arr = (C.c_int * len(kinds))(*[int(k) for k in kinds])
+    ms = C.c_double()
+    _check(lib.rt_spec_precompile(len(kinds), arr, C.byref(ms)), "rt_spec_precompile")
+    return ms.value
 
 
 def Render(scene_or_args, return_stats=False):

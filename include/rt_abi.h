@@ -27,7 +27,9 @@
 #ifndef RT_ABI_H
 #define RT_ABI_H
 
+#ifndef __HIPCC_RTC__ /* hipRTC (scene specialisation) provides size_t itself */
 #include <stddef.h>
+#endif
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -245,6 +247,26 @@ int rt_read_stats(rt_context *ctx, void *stream, int reset, rt_stats *out);
 /* Device time (ms) of the most recent rt_render_rows_async on this context,
  * measured with HIP events on the stream it was launched on. Synchronises. */
 int rt_last_kernel_ms(rt_context *ctx, double *ms_out);
+
+/* Scene specialisation (MI355X-specific, no reference counterpart). With
+ * enable != 0 the context compiles, through hipRTC, a variant of the render
+ * kernel with the current and every later scene's object count and primitive
+ * kinds as compile-time constants, when the scene is small and linear (at most
+ * 8 objects, no BVH, no CSG, scene resident in LDS); other scenes keep the
+ * generic kernel. Output is bit-identical either way; the one-off compile
+ * (seconds, cached per process) pays off for scenes rendered many times.
+ * Returns RT_E_DEVICE with the compiler log if hipRTC is unavailable or fails.
+ * Takes effect immediately for the current scene and in every rt_set_scene. */
+int rt_set_specialize(rt_context *ctx, int enable);
+
+/* Whether the current scene runs a specialised kernel, and the compile time
+ * (ms) that preparing it cost (0 on a cache hit). Either pointer may be NULL. */
+int rt_specialized(rt_context *ctx, int *active, double *compile_ms);
+
+/* Compile (no device needed) and cache, for this process, the specialised
+ * kernel for a scene of nobj (1..8) objects of the given kinds in object
+ * order, e.g. to move the compile out of a latency-critical rt_set_scene. */
+int rt_spec_precompile(int nobj, const int *kinds, double *compile_ms);
 
 /* Diagnostic (tests): run surface program `program` of the context's scene on
  * n (face, u, v) inputs on the device; out10 receives n x 10 Material fields

@@ -458,3 +458,65 @@ def test_dice_program_matches_oracle(ctx):
     ref, ost = oracle_bind.render_rows(packed)
     assert_same(img, ref, "dice")
     assert st.as_dict() == ost.as_dict()
+
+
+# --- scene specialisation (rt_set_specialize): hipRTC-compiled kernel with the
+# object kinds as compile-time constants; must be bit-identical to the generic
+# kernel and the oracle, counters included.
+
+@pytest.fixture(scope="module")
+def spec_ctx():
+    import torch
+    assert torch.cuda.is_available()
+    c = rt.RenderContext(0, specialize=True)
+    yield c
+    c.close()
+
+
+def _spec_case(case):
+    if case in ("c1", "c2", "c3", "canned"):
+        return rt.configs.CONFIGS[case](width=160, height=96)
+    if case == "mixed":
+        return _mixed_scene(1, 5, 96, 64)
+    if case == "ext":
+        return _mixed_scene(41, 3, 96, 64, ext=True)
+    args = _gml_args(case)[0]  # closure-surface programs: sphere, cube
+    args.width, args.height = 128, 96
+    return args
+
+
+@pytest.mark.parametrize("case", ["c1", "c2", "c3", "canned", "mixed", "ext", "sphere", "cube"])
+def test_specialised_kernel_matches_oracle(spec_ctx, case):
+    packed = rt.scene.convert(_spec_case(case))
+    assert packed.scene.num_objects <= 8
+    img, st = render(spec_ctx, packed)
+    active, _ = spec_ctx.specialized()
+    assert active, "scene of %d objects should run the specialised kernel" % packed.scene.num_objects
+    ref, ost = oracle_bind.render_rows(packed)
+    assert_same(img, ref, "specialised " + case)
+    assert st.as_dict() == ost.as_dict()
+
+
+def test_specialisation_skips_large_and_bvh_scenes(spec_ctx):
+    for seed, n in [(2, 11), (4, 40)]:  # 15 objects (linear), 40+ (BVH)
+        packed = rt.scene.convert(_mixed_scene(seed, n, 64, 48))
+        img, st = render(spec_ctx, packed)
+        assert spec_ctx.specialized() == (False, 0.0)
+        ref, ost = oracle_bind.render_rows(packed)
+        assert_same(img, ref, "generic fallback seed %d" % seed)
+        assert st.as_dict() == ost.as_dict()
+
+
+def test_specialised_full_4k_c3_equals_generic(ctx, spec_ctx):
+    packed = rt.scene.convert(rt.configs.c3())
+    a, sa = render(ctx, packed)
+    b, sb = render(spec_ctx, packed)
+    assert spec_ctx.specialized()[0]
+    assert np.array_equal(a, b)
+    assert sa.as_dict() == sb.as_dict()
+    spec_ctx.set_specialize(False)  # switching off takes effect for the current scene
+    assert spec_ctx.specialized() == (False, 0.0)
+    c, _ = render(spec_ctx, packed)
+    assert np.array_equal(a, c)
+    spec_ctx.set_specialize(True)
+    assert spec_ctx.specialized() == (True, 0.0)  # cached: no second compile

@@ -1,0 +1,23 @@
+"""Scene specialisation compile path (hipRTC, no device needed): the embedded
+device sources compile for gfx950 with compile-time object kinds, and bad
+requests fail loudly. Device parity of the specialised kernel is in
+test_gpu_parity.py (test_specialised_*)."""
+import pytest
+
+import go_raytracer_amd as rt
+
+A = rt.abi
+
+
+@pytest.mark.parametrize("kinds", [[A.RT_SPHERE, A.RT_CUBE, A.RT_CYLINDER, A.RT_PLANE],  # C2/C3 shape
+                                   [A.RT_CONE], [A.RT_PLANE] * 8])
+def test_precompile_builds_a_code_object(kinds):
+    ms = rt.spec_precompile(kinds)
+    assert ms >= 0
+    assert rt.spec_precompile(kinds) == 0.0  # cached per process
+
+
+@pytest.mark.parametrize("kinds", [[], [A.RT_SPHERE] * 9, [A.RT_CSG], [7], [-1]])
+def test_precompile_rejects_bad_requests(kinds):
+    with pytest.raises(rt.render.RenderError):
+        rt.spec_precompile(kinds)
