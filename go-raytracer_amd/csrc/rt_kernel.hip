@@ -236,6 +236,7 @@ struct DevScene {
   char* accel = nullptr;
   bool use_bvh = false;
   int nplanes = 0, nnodes = 0, kind_mask = 0;
+  int light_mask = 0;  // bit k: the scene has lights of kind k (RT_LIGHT_*)
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0;
 };
 
@@ -488,6 +489,8 @@ int upload(T** dst, const std::vector<T>& src) {
 // modules per (device, key).
 // ---------------------------------------------------------------------------
 enum { SPEC_MAX_OBJ = 8 };
+static_assert(SF_VM == RT_SPEC_SURFACES && SF_LDIR == RT_SPEC_DIRECTIONAL && SF_LSPOT == RT_SPEC_SPOT,
+              "feature bits of rt_render.h and include/rt_abi.h");
 
 struct Rtc {
   bool tried = false;
@@ -556,7 +559,9 @@ std::string spec_key(const DevScene& s) {
   if (s.use_bvh || s.has_csg || s.nobj < 1 || s.nobj > SPEC_MAX_OBJ || s.blob_bytes > (int)LDS_MAX_BYTES) return "";
   std::string k = std::to_string(s.nobj) + ":";
   for (int i = 0; i < s.nobj; i++) k += (i ? "," : "") + std::to_string(s.kinds[i]);
-  return k;
+  const int feat = (s.num_programs ? SF_VM : 0) | ((s.light_mask >> RT_LIGHT_DIRECTIONAL) & 1 ? SF_LDIR : 0) |
+                   ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
+  return k + ":" + std::to_string(feat);
 }
 
 // Compile the code object for `key` into g_spec_code (no device needed).
@@ -566,11 +571,28 @@ int spec_compile(const std::string& key, double* ms) {
   if (g_spec_code.count(key)) return RT_OK;
   if (!rtc_load()) return fail(RT_E_DEVICE, "scene specialisation: " + g_rtc.err);
   const auto t0 = std::chrono::steady_clock::now();
-  const size_t colon = key.find(':');
-  const std::string d_nobj = "-DRT_SPEC_NOBJ=" + key.substr(0, colon);
-  const std::string d_kinds = "-DRT_SPEC_KINDS=" + key.substr(colon + 1);
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", d_nobj.c_str(),
-                        d_kinds.c_str()};
+  // key = "nobj:kind,kind,...:features"
+  const size_t c1 = key.find(':'), c2 = key.rfind(':');
+  const std::string d_nobj = "-DRT_SPEC_NOBJ=" + key.substr(0, c1);
+  const std::string d_kinds = "-DRT_SPEC_KINDS=" + key.substr(c1 + 1, c2 - c1 - 1);
+  const std::string d_feat = "-DRT_SPEC_FEAT=" + key.substr(c2 + 1);
+  std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                                   d_nobj.c_str(), d_kinds.c_str(), d_feat.c_str()};
+  // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only)
+  std::vector<std::string> extra;
+  if (const char* e = getenv("RT_SPEC_EXTRA_FLAGS")) {
+    std::string cur;
+    for (const char* q = e;; q++) {
+      if (*q == ' ' || *q == 0) {
+        if (!cur.empty()) extra.push_back(cur);
+        cur.clear();
+        if (!*q) break;
+      } else {
+        cur += *q;
+      }
+    }
+  }
+  for (const auto& x : extra) opts.push_back(x.c_str());
   const char* name_expr = "rt_render_kernel<true, false, false>";
   hiprtcProgram prog;
   hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
@@ -579,7 +601,7 @@ int spec_compile(const std::string& key, double* ms) {
   SpecCode sc;
   std::string msg;
   r = g_rtc.add_name(prog, name_expr);
-  if (r == HIPRTC_SUCCESS) r = g_rtc.compile(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  if (r == HIPRTC_SUCCESS) r = g_rtc.compile(prog, (int)opts.size(), opts.data());
   if (r != HIPRTC_SUCCESS) {
     size_t n = 0;
     std::string log;
@@ -651,8 +673,9 @@ int rt_set_specialize(rt_context* c, int enable) {
   return spec_prepare(c);
 }
 
-int rt_spec_precompile(int nobj, const int* kinds, double* compile_ms) {
+int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile_ms) {
   if (compile_ms) *compile_ms = 0;
+  if (features & ~(SF_VM | SF_LDIR | SF_LSPOT)) return fail(RT_E_INVALID, "rt_spec_precompile: unknown feature bits");
   if (nobj < 1 || nobj > SPEC_MAX_OBJ || !kinds) return fail(RT_E_INVALID, "rt_spec_precompile: 1..8 objects");
   std::string key = std::to_string(nobj) + ":";
   for (int i = 0; i < nobj; i++) {
@@ -660,6 +683,7 @@ int rt_spec_precompile(int nobj, const int* kinds, double* compile_ms) {
       return fail(RT_E_INVALID, "rt_spec_precompile: bad primitive kind");
     key += (i ? "," : "") + std::to_string(kinds[i]);
   }
+  key += ":" + std::to_string(features);
   std::lock_guard<std::mutex> lock(g_spec_mu);
   double ms = 0;
   int rc = spec_compile(key, &ms);
@@ -998,11 +1022,13 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
         L[k] = in->lights[l].position[k];
         L[3 + k] = in->lights[l].color[k];
       }
+      s.light_mask |= 1 << RT_LIGHT_POINT;
       continue;
     }
     // contest-extension lights (oracle/rt_oracle.c convert_scene)
     const rt_light& e = in->ext_lights[l];
     if (e.kind < RT_LIGHT_POINT || e.kind > RT_LIGHT_SPOT) return fail(RT_E_INVALID, "unknown light kind");
+    s.light_mask |= 1 << e.kind;
     for (int k = 0; k < 3; k++) {
       L[k] = e.position[k];
       L[3 + k] = e.color[k];

@@ -659,6 +659,28 @@ __device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ?
 // Frame flags (packed with the material index).
 enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16 };
 
+// Scene specialisation (hipRTC build, see rt_kernel.hip spec_compile): the
+// object kinds and the scene features below are compile-time constants, so
+// branches for kinds, surface programs and light kinds the scene lacks fold
+// away. The generic build keeps every branch (all bits set).
+enum { SF_VM = 1, SF_LDIR = 2, SF_LSPOT = 4 };  // closure surfaces, directional / spot lights
+#ifdef RT_SPEC_NOBJ
+constexpr int spec_kinds[RT_SPEC_NOBJ] = {RT_SPEC_KINDS};
+constexpr int spec_kind_mask() {
+  int m = 0;
+  for (int i = 0; i < RT_SPEC_NOBJ; i++) m |= 1 << spec_kinds[i];
+  return m;
+}
+constexpr int SPEC_KMASK = spec_kind_mask();
+constexpr int SPEC_FEAT = RT_SPEC_FEAT;
+#else
+constexpr int SPEC_KMASK = -1;
+constexpr int SPEC_FEAT = -1;
+#endif
+// May the scene hold objects of kind k / use feature f?
+__device__ constexpr bool spec_kind(int k) { return ((SPEC_KMASK >> k) & 1) != 0; }
+__device__ constexpr bool spec_feat(int f) { return (SPEC_FEAT & f) != 0; }
+
 // ---------------------------------------------------------------------------
 // Closure-surface VM: executes a straight-line register
 // program compiled on the host from a GML surface function
@@ -949,7 +971,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             }
             d3 fcol;
             double frefl;
-            if (fl & FL_VMMAT) {
+            if (spec_feat(SF_VM) && (fl & FL_VMMAT)) {
               fcol = ld3(f, 14);
               frefl = f[17 * 64];
             } else {
@@ -1080,9 +1102,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if constexpr (!BVH) {
 #ifdef RT_SPEC_NOBJ
         {
-          constexpr int spec_k[RT_SPEC_NOBJ] = {RT_SPEC_KINDS};
 #pragma unroll
-          for (int i = 0; i < RT_SPEC_NOBJ; i++) trace_obj(i, spec_k[i], S.geo + (size_t)i * GEO, tr);
+          for (int i = 0; i < RT_SPEC_NOBJ; i++) trace_obj(i, spec_kinds[i], S.geo + (size_t)i * GEO, tr);
         }
 #else
         for (int i = 0; i < P.nobj; i++) trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
@@ -1187,9 +1208,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       d3 p = add(l.o, scale(l.d, hit_t));  // Hit.PointObj
       pw = mk(s[0] * p.x + s[1] * p.y + s[2] * p.z + s[3], s[4] * p.x + s[5] * p.y + s[6] * p.z + s[7],
               s[8] * p.x + s[9] * p.y + s[10] * p.z + s[11]);
-      if (k == RT_SPHERE) {
+      if (spec_kind(RT_SPHERE) && k == RT_SPHERE) {
         nw = p;
-      } else if (k == RT_CYLINDER || k == RT_CONE) {
+      } else if ((spec_kind(RT_CYLINDER) && k == RT_CYLINDER) || (spec_kind(RT_CONE) && k == RT_CONE)) {
         d3 n = sf == 0 ? (k == RT_CONE ? mk(p.x, -p.y, p.z) : mk(p.x, 0, p.z)) : (sf == 1 ? mk(0, 1, 0) : mk(0, -1, 0));
         // NormalMat = WorldToObject^T (raytracer.go:814): MulDir then Normalize.
         nw = norm(mk(g[0] * n.x + g[4] * n.y + g[8] * n.z, g[1] * n.x + g[5] * n.y + g[9] * n.z,
@@ -1199,7 +1220,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       }
       if (flip) nw = neg(nw);  // the composite's outward normal
       mat = S.objmat[(size_t)si * OMAT + sf];
-      if (mat < 0) {
+      if (spec_feat(SF_VM) && mat < 0) {
         // Closure surface: (face, u, v) as ComputeSurfaceProps computes them
         // (raytracer.go:124-150, 196-205, 249, 339-359), then the VM.
         double u, v;
@@ -1245,7 +1266,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 
     // computeLighting + inShadow (raytracer.go:372-429)
     PH_MARK(3);
-    const double* M = mat >= 0 ? S.mats + (size_t)mat * MAT : vmrec;
+    const double* M = (!spec_feat(SF_VM) || mat >= 0) ? S.mats + (size_t)mat * MAT : vmrec;
     d3 L = mk(0, 0, 0);
     if (hit) L = scale(mk(G[0], G[1], G[2]), M[9]);
     const double rlen = len(ray.d);
@@ -1256,7 +1277,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       const int lkind = (int)lt[9];  // wave-uniform
       d3 ldir;
       double dist;
-      if (lkind == RT_LIGHT_DIRECTIONAL) {  // extension: light at infinity
+      if (spec_feat(SF_LDIR) && lkind == RT_LIGHT_DIRECTIONAL) {  // extension: light at infinity
         ldir = mk(lt[6], lt[7], lt[8]);
         dist = __builtin_inf();
       } else {
@@ -1277,11 +1298,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       int send = P.nobj;
       if constexpr (!BVH) {
 #ifdef RT_SPEC_NOBJ
-        constexpr int spec_k2[RT_SPEC_NOBJ] = {RT_SPEC_KINDS};
 #pragma unroll
         for (int i = 0; i < RT_SPEC_NOBJ; i++) {
           if (!__any(open)) break;
-          const int k = spec_k2[i];
+          const int k = spec_kinds[i];
 #else
         for (int i = 0; i < P.nobj; i++) {
           if (!__any(open)) break;
@@ -1406,13 +1426,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         sc1 += pe.y - (hk == 1 ? 1u : 0u);
         sc2 += pe.z - (hk == 2 ? 1u : 0u);
         sc3 += pe.w - (hk == 3 ? 1u : 0u);
-        if (P.kind_mask & 16) cnt_add(CNT_ST0 + 4, pe4 - (hk == 4 ? 1u : 0u));  // cones, CSG: rare, flushed per light
-        if (P.kind_mask & 32) cnt_add(CNT_ST0 + 5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
+        if (spec_kind(4) && (P.kind_mask & 16)) cnt_add(CNT_ST0 + 4, pe4 - (hk == 4 ? 1u : 0u));  // cones, CSG: rare, flushed per light
+        if (spec_kind(5) && (P.kind_mask & 32)) cnt_add(CNT_ST0 + 5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
       }
       PH_MARK(4);
       if (hit && open) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
-        if (lkind == RT_LIGHT_SPOT) {  // extension: cone falloff
+        if (spec_feat(SF_LSPOT) && lkind == RT_LIGHT_SPOT) {  // extension: cone falloff
           const double ca = dot(neg(ldir), mk(lt[6], lt[7], lt[8]));
           lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11]) : 0.0);
         }
@@ -1426,10 +1446,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       PH_MARK(5);
     }
     if (hit) {
-      if (P.kind_mask & 1) cnt_add(CNT_ST0 + 0, sc0);
-      if (P.kind_mask & 2) cnt_add(CNT_ST0 + 1, sc1);
-      if (P.kind_mask & 4) cnt_add(CNT_ST0 + 2, sc2);
-      if (P.kind_mask & 8) cnt_add(CNT_ST0 + 3, sc3);
+      if (spec_kind(0) && (P.kind_mask & 1)) cnt_add(CNT_ST0 + 0, sc0);
+      if (spec_kind(1) && (P.kind_mask & 2)) cnt_add(CNT_ST0 + 1, sc1);
+      if (spec_kind(2) && (P.kind_mask & 4)) cnt_add(CNT_ST0 + 2, sc2);
+      if (spec_kind(3) && (P.kind_mask & 8)) cnt_add(CNT_ST0 + 3, sc3);
     }
 
     // traceRay body after lighting (raytracer.go:505-561)
@@ -1499,7 +1519,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             st3(f, 9, trr.d);
           }
           core_st(sp, 3, kr);
-          if (mat < 0) {  // the VM record is per lane: keep what the combine needs
+          if (spec_feat(SF_VM) && mat < 0) {  // the VM record is per lane: keep what the combine needs
             double* f = frame_ptr(stk, sp);
             st3(f, 14, col);
             f[17 * 64] = refl;

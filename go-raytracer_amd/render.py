@@ -63,7 +63,7 @@ def load_library(path=None):
     l.rt_set_specialize.restype = i
     l.rt_specialized.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
     l.rt_specialized.restype = i
-    l.rt_spec_precompile.argtypes = [i, C.POINTER(i), C.POINTER(C.c_double)]
+    l.rt_spec_precompile.argtypes = [i, C.POINTER(i), i, C.POINTER(C.c_double)]
     l.rt_spec_precompile.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
     l.rt_render.restype = i
@@ -215,14 +215,15 @@ class RenderContext:
         return out.cpu().numpy()
 
 
-def spec_precompile(kinds):
+def spec_precompile(kinds, features=0):
     """Compile (no device needed) the specialised kernel for a scene whose
-    objects have these primitive kinds, in order; returns the compile time (ms,
-    0 if already cached in this process)."""
+    objects have these primitive kinds, in order, and RT_SPEC_* feature bits
+    (abi.RT_SPEC_SURFACES / _DIRECTIONAL / _SPOT); returns the compile time
+    (ms, 0 if already cached in this process)."""
     lib = load_library()
     arr = (C.c_int * len(kinds))(*[int(k) for k in kinds])
     ms = C.c_double()
-    _check(lib.rt_spec_precompile(len(kinds), arr, C.byref(ms)), "rt_spec_precompile")
+    _check(lib.rt_spec_precompile(len(kinds), arr, int(features), C.byref(ms)), "rt_spec_precompile")
     return ms.value
 
 

@@ -265,8 +265,12 @@ int rt_specialized(rt_context *ctx, int *active, double *compile_ms);
 
 /* Compile (no device needed) and cache, for this process, the specialised
  * kernel for a scene of nobj (1..8) objects of the given kinds in object
- * order, e.g. to move the compile out of a latency-critical rt_set_scene. */
-int rt_spec_precompile(int nobj, const int *kinds, double *compile_ms);
+ * order and the given RT_SPEC_* feature bits, e.g. to move the compile out of
+ * a latency-critical rt_set_scene. */
+#define RT_SPEC_SURFACES 1    /* the scene has closure (surface program) materials */
+#define RT_SPEC_DIRECTIONAL 2 /* ... directional lights */
+#define RT_SPEC_SPOT 4        /* ... spot lights */
+int rt_spec_precompile(int nobj, const int *kinds, int features, double *compile_ms);
 
 /* Diagnostic (tests): run surface program `program` of the context's scene on
  * n (face, u, v) inputs on the device; out10 receives n x 10 Material fields

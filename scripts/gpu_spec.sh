@@ -9,3 +9,4 @@ for cfg in c3 c2; do
     timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 --cpu-baseline off --specialize $sp > gpurun_out/bench_${cfg}_$sp.json 2> gpurun_out/bench_${cfg}_$sp.err || exit 1
   done
 done
+RT_SPEC_EXTRA_FLAGS=-DRT_MIN_WAVES=4 timeout -k 10 300 python bench.py --config c3 --steps 20 --warmup 3 --cpu-baseline off > gpurun_out/bench_c3_w4.json 2> gpurun_out/bench_c3_w4.err || exit 1

@@ -9,15 +9,23 @@ import go_raytracer_amd as rt
 A = rt.abi
 
 
-@pytest.mark.parametrize("kinds", [[A.RT_SPHERE, A.RT_CUBE, A.RT_CYLINDER, A.RT_PLANE],  # C2/C3 shape
-                                   [A.RT_CONE], [A.RT_PLANE] * 8])
-def test_precompile_builds_a_code_object(kinds):
-    ms = rt.spec_precompile(kinds)
+@pytest.mark.parametrize("kinds,feat", [
+    ([A.RT_SPHERE, A.RT_CUBE, A.RT_CYLINDER, A.RT_PLANE], 0),  # C2/C3 shape
+    ([A.RT_CONE, A.RT_SPHERE], A.RT_SPEC_DIRECTIONAL | A.RT_SPEC_SPOT),
+    ([A.RT_CUBE], A.RT_SPEC_SURFACES),
+    ([A.RT_PLANE] * 8, 7)])
+def test_precompile_builds_a_code_object(kinds, feat):
+    ms = rt.spec_precompile(kinds, feat)
     assert ms >= 0
-    assert rt.spec_precompile(kinds) == 0.0  # cached per process
+    assert rt.spec_precompile(kinds, feat) == 0.0  # cached per process
 
 
 @pytest.mark.parametrize("kinds", [[], [A.RT_SPHERE] * 9, [A.RT_CSG], [7], [-1]])
 def test_precompile_rejects_bad_requests(kinds):
     with pytest.raises(rt.render.RenderError):
         rt.spec_precompile(kinds)
+
+
+def test_precompile_rejects_unknown_feature_bits():
+    with pytest.raises(rt.render.RenderError):
+        rt.spec_precompile([A.RT_SPHERE], 8)
