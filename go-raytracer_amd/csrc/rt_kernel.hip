@@ -553,31 +553,51 @@ bool rtc_load() {
   return true;
 }
 
-// Specialisation key of a scene, or "" when the scene runs the generic kernel
-// (BVH or CSG flavour, scene not LDS-resident, no or too many objects).
-std::string spec_key(const DevScene& s) {
-  if (s.use_bvh || s.has_csg || s.nobj < 1 || s.nobj > SPEC_MAX_OBJ || s.blob_bytes > (int)LDS_MAX_BYTES) return "";
-  std::string k = std::to_string(s.nobj) + ":";
-  for (int i = 0; i < s.nobj; i++) k += (i ? "," : "") + std::to_string(s.kinds[i]);
-  const int feat = (s.num_programs ? SF_VM : 0) | ((s.light_mask >> RT_LIGHT_DIRECTIONAL) & 1 ? SF_LDIR : 0) |
-                   ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
-  return k + ":" + std::to_string(feat);
+// What a specialised kernel is compiled for. Serialised as the cache key
+// "lds:bvh:nobj:kinds:kmask:feat"; nobj > 0 (kinds = "k0,k1,...") unrolls the
+// object loops of a small linear LDS scene, nobj = 0 only fixes the kind mask
+// and the feature bits (BVH, global-memory and larger linear scenes).
+struct SpecKey {
+  int lds = 1, bvh = 0, nobj = 0;
+  std::string kinds;
+  int kmask = 0, feat = 0;
+  std::string str() const {
+    return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
+           std::to_string(kmask) + ":" + std::to_string(feat);
+  }
+};
+
+// Specialisation of a scene; false when it runs the generic kernel (CSG
+// flavour or no objects).
+bool spec_key(const DevScene& s, SpecKey* k) {
+  if (s.has_csg || s.nobj < 1) return false;
+  k->lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
+  k->bvh = s.use_bvh;
+  k->nobj = (!s.use_bvh && k->lds && s.nobj <= SPEC_MAX_OBJ) ? s.nobj : 0;
+  k->kinds.clear();
+  for (int i = 0; i < k->nobj; i++) k->kinds += (i ? "," : "") + std::to_string(s.kinds[i]);
+  k->kmask = s.kind_mask;
+  k->feat = (s.num_programs ? SF_VM : 0) | ((s.light_mask >> RT_LIGHT_DIRECTIONAL) & 1 ? SF_LDIR : 0) |
+            ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
+  return true;
 }
 
 // Compile the code object for `key` into g_spec_code (no device needed).
 // Caller holds g_spec_mu.
-int spec_compile(const std::string& key, double* ms) {
+int spec_compile(const SpecKey& sk, double* ms) {
   *ms = 0;
+  const std::string key = sk.str();
   if (g_spec_code.count(key)) return RT_OK;
   if (!rtc_load()) return fail(RT_E_DEVICE, "scene specialisation: " + g_rtc.err);
   const auto t0 = std::chrono::steady_clock::now();
-  // key = "nobj:kind,kind,...:features"
-  const size_t c1 = key.find(':'), c2 = key.rfind(':');
-  const std::string d_nobj = "-DRT_SPEC_NOBJ=" + key.substr(0, c1);
-  const std::string d_kinds = "-DRT_SPEC_KINDS=" + key.substr(c1 + 1, c2 - c1 - 1);
-  const std::string d_feat = "-DRT_SPEC_FEAT=" + key.substr(c2 + 1);
-  std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                                   d_nobj.c_str(), d_kinds.c_str(), d_feat.c_str()};
+  std::vector<std::string> defs = {"-DRT_SPEC_KMASK=" + std::to_string(sk.kmask),
+                                   "-DRT_SPEC_FEAT=" + std::to_string(sk.feat)};
+  if (sk.nobj > 0) {
+    defs.push_back("-DRT_SPEC_NOBJ=" + std::to_string(sk.nobj));
+    defs.push_back("-DRT_SPEC_KINDS=" + sk.kinds);
+  }
+  std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
+  for (const auto& d : defs) opts.push_back(d.c_str());
   // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only)
   std::vector<std::string> extra;
   if (const char* e = getenv("RT_SPEC_EXTRA_FLAGS")) {
@@ -593,7 +613,9 @@ int spec_compile(const std::string& key, double* ms) {
     }
   }
   for (const auto& x : extra) opts.push_back(x.c_str());
-  const char* name_expr = "rt_render_kernel<true, false, false>";
+  const std::string name = std::string("rt_render_kernel<") + (sk.lds ? "true" : "false") + ", " +
+                           (sk.bvh ? "true" : "false") + ", false>";
+  const char* name_expr = name.c_str();
   hiprtcProgram prog;
   hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
                                 k_jit_names);
@@ -630,14 +652,15 @@ int spec_compile(const std::string& key, double* ms) {
 
 // Compile (or fetch) the specialised LDS/linear kernel for `key` on `device`.
 // Caller holds g_spec_mu.
-int spec_build(int device, const std::string& key, hipFunction_t* fn, double* ms) {
+int spec_build(int device, const SpecKey& sk, hipFunction_t* fn, double* ms) {
   *ms = 0;
+  const std::string key = sk.str();
   auto fit = g_spec_fn.find({device, key});
   if (fit != g_spec_fn.end()) {
     *fn = fit->second;
     return RT_OK;
   }
-  int rc = spec_compile(key, ms);
+  int rc = spec_compile(sk, ms);
   if (rc != RT_OK) return rc;
   const SpecCode& sc = g_spec_code.at(key);
   DeviceGuard guard(device);
@@ -655,10 +678,10 @@ int spec_prepare(rt_context* c) {
   c->spec_fn = nullptr;
   c->spec_ms = 0;
   if (!c->specialize || !c->has_scene) return RT_OK;
-  const std::string key = spec_key(c->sc);
-  if (key.empty()) return RT_OK;
+  SpecKey sk;
+  if (!spec_key(c->sc, &sk)) return RT_OK;
   std::lock_guard<std::mutex> lock(g_spec_mu);
-  return spec_build(c->device, key, &c->spec_fn, &c->spec_ms);
+  return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
 }
 
 }  // namespace
@@ -677,16 +700,18 @@ int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile
   if (compile_ms) *compile_ms = 0;
   if (features & ~(SF_VM | SF_LDIR | SF_LSPOT)) return fail(RT_E_INVALID, "rt_spec_precompile: unknown feature bits");
   if (nobj < 1 || nobj > SPEC_MAX_OBJ || !kinds) return fail(RT_E_INVALID, "rt_spec_precompile: 1..8 objects");
-  std::string key = std::to_string(nobj) + ":";
+  SpecKey sk;
+  sk.nobj = nobj;
   for (int i = 0; i < nobj; i++) {
     if (kinds[i] < 0 || kinds[i] >= RT_NUM_KINDS || kinds[i] == RT_CSG)
       return fail(RT_E_INVALID, "rt_spec_precompile: bad primitive kind");
-    key += (i ? "," : "") + std::to_string(kinds[i]);
+    sk.kinds += (i ? "," : "") + std::to_string(kinds[i]);
+    sk.kmask |= 1 << kinds[i];
   }
-  key += ":" + std::to_string(features);
+  sk.feat = features;
   std::lock_guard<std::mutex> lock(g_spec_mu);
   double ms = 0;
-  int rc = spec_compile(key, &ms);
+  int rc = spec_compile(sk, &ms);
   if (compile_ms) *compile_ms = ms;
   return rc;
 }
@@ -1212,7 +1237,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   else
     kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, false> : (const void*)rt_render_kernel<true, false, false>)
               : (s.use_bvh ? (const void*)rt_render_kernel<false, true, false> : (const void*)rt_render_kernel<false, false, false>);
-  hipFunction_t spec = (lds && !s.use_bvh && !s.has_csg) ? c->spec_fn : nullptr;
+  hipFunction_t spec = s.has_csg ? nullptr : c->spec_fn;  // built for this scene's flavour (spec_key)
   int per_cu = 0;
   if (spec) {
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, spec, WG, shmem) != hipSuccess) per_cu = 0;

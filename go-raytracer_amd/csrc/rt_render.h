@@ -43,6 +43,32 @@
 
 using namespace rt;
 
+// Scene specialisation (hipRTC build, see rt_kernel.hip spec_compile): the
+// object kinds and the scene features below are compile-time constants, so
+// branches for kinds, surface programs and light kinds the scene lacks fold
+// away. The generic build keeps every branch (all bits set).
+enum { SF_VM = 1, SF_LDIR = 2, SF_LSPOT = 4 };  // closure surfaces, directional / spot lights
+#ifdef RT_SPEC_NOBJ
+constexpr int spec_kinds[RT_SPEC_NOBJ] = {RT_SPEC_KINDS};
+constexpr int spec_kind_mask() {
+  int m = 0;
+  for (int i = 0; i < RT_SPEC_NOBJ; i++) m |= 1 << spec_kinds[i];
+  return m;
+}
+constexpr int SPEC_KMASK = spec_kind_mask();
+constexpr int SPEC_FEAT = RT_SPEC_FEAT;
+static_assert(SPEC_KMASK == RT_SPEC_KMASK, "RT_SPEC_KINDS and RT_SPEC_KMASK disagree");
+#elif defined(RT_SPEC_KMASK)
+constexpr int SPEC_KMASK = RT_SPEC_KMASK;
+constexpr int SPEC_FEAT = RT_SPEC_FEAT;
+#else
+constexpr int SPEC_KMASK = -1;
+constexpr int SPEC_FEAT = -1;
+#endif
+// May the scene hold objects of kind k / use feature f?
+__device__ constexpr bool spec_kind(int k) { return ((SPEC_KMASK >> k) & 1) != 0; }
+__device__ constexpr bool spec_feat(int f) { return (SPEC_FEAT & f) != 0; }
+
 // ---------------------------------------------------------------------------
 // Scene blob (built by rt_set_scene), one contiguous allocation, 16-B aligned
 // sections; strides in doubles:
@@ -319,16 +345,12 @@ __device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, 
 __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r, double& t, int& face) {
   Ray l = to_obj(g, r);
   face = 0;
-  switch (k) {
-    case RT_SPHERE:
-      return sphere_hit(l, t);
-    case RT_PLANE:
-      return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
-    case RT_CUBE:
-      return cube_hit(l, t, face);
-    default:  // RT_CYLINDER, RT_CONE
-      return quadric_hit(l, t, face, k == RT_CONE);
-  }
+  // (kinds the specialised scene lacks fold away; the generic build keeps all)
+  if (spec_kind(RT_SPHERE) && k == RT_SPHERE) return sphere_hit(l, t);
+  if (spec_kind(RT_PLANE) && k == RT_PLANE) return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
+  if (spec_kind(RT_CUBE) && k == RT_CUBE) return cube_hit(l, t, face);
+  if (!spec_kind(RT_CYLINDER) && !spec_kind(RT_CONE)) return false;  // unreachable for the scene's kinds
+  return quadric_hit(l, t, face, spec_kind(RT_CONE) && (!spec_kind(RT_CYLINDER) || k == RT_CONE));
 }
 
 __device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(__ballot(b)); }
@@ -659,27 +681,6 @@ __device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ?
 // Frame flags (packed with the material index).
 enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16 };
 
-// Scene specialisation (hipRTC build, see rt_kernel.hip spec_compile): the
-// object kinds and the scene features below are compile-time constants, so
-// branches for kinds, surface programs and light kinds the scene lacks fold
-// away. The generic build keeps every branch (all bits set).
-enum { SF_VM = 1, SF_LDIR = 2, SF_LSPOT = 4 };  // closure surfaces, directional / spot lights
-#ifdef RT_SPEC_NOBJ
-constexpr int spec_kinds[RT_SPEC_NOBJ] = {RT_SPEC_KINDS};
-constexpr int spec_kind_mask() {
-  int m = 0;
-  for (int i = 0; i < RT_SPEC_NOBJ; i++) m |= 1 << spec_kinds[i];
-  return m;
-}
-constexpr int SPEC_KMASK = spec_kind_mask();
-constexpr int SPEC_FEAT = RT_SPEC_FEAT;
-#else
-constexpr int SPEC_KMASK = -1;
-constexpr int SPEC_FEAT = -1;
-#endif
-// May the scene hold objects of kind k / use feature f?
-__device__ constexpr bool spec_kind(int k) { return ((SPEC_KMASK >> k) & 1) != 0; }
-__device__ constexpr bool spec_feat(int f) { return (SPEC_FEAT & f) != 0; }
 
 // ---------------------------------------------------------------------------
 // Closure-surface VM: executes a straight-line register

@@ -497,14 +497,33 @@ def test_specialised_kernel_matches_oracle(spec_ctx, case):
     assert st.as_dict() == ost.as_dict()
 
 
-def test_specialisation_skips_large_and_bvh_scenes(spec_ctx):
-    for seed, n in [(2, 11), (4, 40)]:  # 15 objects (linear), 40+ (BVH)
-        packed = rt.scene.convert(_mixed_scene(seed, n, 64, 48))
-        img, st = render(spec_ctx, packed)
-        assert spec_ctx.specialized() == (False, 0.0)
-        ref, ost = oracle_bind.render_rows(packed)
-        assert_same(img, ref, "generic fallback seed %d" % seed)
-        assert st.as_dict() == ost.as_dict()
+@pytest.mark.parametrize("seed,n,ext", [(2, 11, False), (4, 40, False), (5, 150, False), (22, 30, True)])
+def test_specialised_kind_mask_scenes_match_oracle(spec_ctx, seed, n, ext):
+    """> 8 objects (linear) and BVH scenes: kind mask + feature bits only."""
+    packed = rt.scene.convert(_mixed_scene(seed, n, 96, 64, ext=ext))
+    img, st = render(spec_ctx, packed)
+    assert spec_ctx.specialized()[0]
+    ref, ost = oracle_bind.render_rows(packed)
+    assert_same(img, ref, "specialised seed %d n %d" % (seed, n))
+    assert st.as_dict() == ost.as_dict()
+
+
+def test_specialised_c5_rows_match_oracle(spec_ctx):
+    packed = rt.scene.convert(rt.configs.c5(width=96, height=60))
+    spec_ctx.set_scene(packed)
+    assert spec_ctx.specialized()[0]
+    img = spec_ctx.render(20, 40)
+    ref, _ = oracle_bind.render_rows(packed, 20, 40)
+    assert_same(img, ref, "specialised c5 rows")
+
+
+def test_specialisation_skips_csg_scenes(spec_ctx):
+    packed = rt.scene.convert(_csg_scene(32, 4, 64, 48))
+    img, st = render(spec_ctx, packed)
+    assert spec_ctx.specialized() == (False, 0.0)
+    ref, ost = oracle_bind.render_rows(packed)
+    assert_same(img, ref, "csg generic")
+    assert st.as_dict() == ost.as_dict()
 
 
 def test_specialised_full_4k_c3_equals_generic(ctx, spec_ctx):
