@@ -237,6 +237,7 @@ struct DevScene {
   bool use_bvh = false;
   int nplanes = 0, nnodes = 0, kind_mask = 0;
   int light_mask = 0;  // bit k: the scene has lights of kind k (RT_LIGHT_*)
+  int leaf_kind_mask = 0;  // bit k: some CSG leaf has kind k
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0;
 };
 
@@ -554,29 +555,30 @@ bool rtc_load() {
 }
 
 // What a specialised kernel is compiled for. Serialised as the cache key
-// "lds:bvh:nobj:kinds:kmask:feat"; nobj > 0 (kinds = "k0,k1,...") unrolls the
+// "lds:bvh:csg:nobj:kinds:kmask:feat"; nobj > 0 (kinds = "k0,k1,...") unrolls the
 // object loops of a small linear LDS scene, nobj = 0 only fixes the kind mask
 // and the feature bits (BVH, global-memory and larger linear scenes).
 struct SpecKey {
-  int lds = 1, bvh = 0, nobj = 0;
+  int lds = 1, bvh = 0, csg = 0, nobj = 0;
   std::string kinds;
   int kmask = 0, feat = 0;
   std::string str() const {
-    return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
+    return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
            std::to_string(kmask) + ":" + std::to_string(feat);
   }
 };
 
-// Specialisation of a scene; false when it runs the generic kernel (CSG
-// flavour or no objects).
+// Specialisation of a scene; false when it runs the generic kernel (no
+// objects).
 bool spec_key(const DevScene& s, SpecKey* k) {
-  if (s.has_csg || s.nobj < 1) return false;
+  if (s.nobj < 1) return false;
   k->lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
   k->bvh = s.use_bvh;
-  k->nobj = (!s.use_bvh && k->lds && s.nobj <= SPEC_MAX_OBJ) ? s.nobj : 0;
+  k->csg = s.has_csg;
+  k->nobj = (!s.use_bvh && !s.has_csg && k->lds && s.nobj <= SPEC_MAX_OBJ) ? s.nobj : 0;
   k->kinds.clear();
   for (int i = 0; i < k->nobj; i++) k->kinds += (i ? "," : "") + std::to_string(s.kinds[i]);
-  k->kmask = s.kind_mask;
+  k->kmask = s.kind_mask | s.leaf_kind_mask;  // CSG leaves are shaded by their own kind
   k->feat = (s.num_programs ? SF_VM : 0) | ((s.light_mask >> RT_LIGHT_DIRECTIONAL) & 1 ? SF_LDIR : 0) |
             ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
   return true;
@@ -614,7 +616,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   }
   for (const auto& x : extra) opts.push_back(x.c_str());
   const std::string name = std::string("rt_render_kernel<") + (sk.lds ? "true" : "false") + ", " +
-                           (sk.bvh ? "true" : "false") + ", false>";
+                           (sk.bvh ? "true" : "false") + ", " + (sk.csg ? "true" : "false") + ">";
   const char* name_expr = name.c_str();
   hiprtcProgram prog;
   hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
@@ -1168,6 +1170,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       b.leaf_geo.clear();
     }
     for (int i = 0; i < s.nobj; i++) s.kind_mask |= 1 << kind[i];
+    for (int i = s.nobj; i < ntot; i++) s.leaf_kind_mask |= 1 << kind[i];
     s.off_nodes = 0;
     s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
     s.off_planes = s.off_bobj + ((b.leaf_geo.size() * sizeof(double) + 15) & ~(size_t)15);
@@ -1237,7 +1240,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   else
     kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, false> : (const void*)rt_render_kernel<true, false, false>)
               : (s.use_bvh ? (const void*)rt_render_kernel<false, true, false> : (const void*)rt_render_kernel<false, false, false>);
-  hipFunction_t spec = s.has_csg ? nullptr : c->spec_fn;  // built for this scene's flavour (spec_key)
+  hipFunction_t spec = c->spec_fn;  // built for this scene's flavour (spec_key)
   int per_cu = 0;
   if (spec) {
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, spec, WG, shmem) != hipSuccess) per_cu = 0;

@@ -419,7 +419,7 @@ __device__ __forceinline__ void leaf_interval(int kind, const double* g, const R
   b = __builtin_inf();
   int fa = 0, fb = 0;
   bool ok = true;
-  if (kind == RT_SPHERE) {
+  if (spec_kind(RT_SPHERE) && kind == RT_SPHERE) {
     const double qa = dot(l.d, l.d), hb = dot(l.o, l.d), c = dot(l.o, l.o) - 1.0;
     const double disc = hb * hb - qa * c;
     if (disc < 0.0) {
@@ -429,7 +429,7 @@ __device__ __forceinline__ void leaf_interval(int kind, const double* g, const R
       a = (-hb - sq) / qa;
       b = (-hb + sq) / qa;
     }
-  } else if (kind == RT_CUBE) {
+  } else if (spec_kind(RT_CUBE) && kind == RT_CUBE) {
     const double o3[3] = {l.o.x, l.o.y, l.o.z}, d3v[3] = {l.d.x, l.d.y, l.d.z};
     const int flo[3] = {2, 5, 0}, fhi[3] = {3, 4, 1};
 #pragma unroll
@@ -457,7 +457,7 @@ __device__ __forceinline__ void leaf_interval(int kind, const double* g, const R
       }
     }
     if (a > b) ok = false;
-  } else if (kind == RT_CYLINDER) {
+  } else if (spec_kind(RT_CYLINDER) && kind == RT_CYLINDER) {
     const double qa = l.d.x * l.d.x + l.d.z * l.d.z;
     if (qa > 1e-12) {
       const double hb = l.o.x * l.d.x + l.o.z * l.d.z;

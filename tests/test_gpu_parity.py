@@ -517,12 +517,13 @@ def test_specialised_c5_rows_match_oracle(spec_ctx):
     assert_same(img, ref, "specialised c5 rows")
 
 
-def test_specialisation_skips_csg_scenes(spec_ctx):
-    packed = rt.scene.convert(_csg_scene(32, 4, 64, 48))
+@pytest.mark.parametrize("seed,n_extra", [(31, 0), (33, 20)])
+def test_specialised_csg_scenes_match_oracle(spec_ctx, seed, n_extra):
+    packed = rt.scene.convert(_csg_scene(seed, n_extra, 80, 60))
     img, st = render(spec_ctx, packed)
-    assert spec_ctx.specialized() == (False, 0.0)
+    assert spec_ctx.specialized()[0]
     ref, ost = oracle_bind.render_rows(packed)
-    assert_same(img, ref, "csg generic")
+    assert_same(img, ref, "specialised csg seed %d" % seed)
     assert st.as_dict() == ost.as_dict()
 
 
