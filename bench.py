@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Benchmark of the render hot path (BASELINE.json metric: Mrays/s at 4K depth 6).
 
-One step = one full frame of the workload, rows sharded across the N ranks
-(one process per GPU, RCCL gather of the bands to rank 0). N=1 workload =
-config C3 (3840x2160, depth 6, cylinder + cube + sphere-for-cone, 4 lights).
+One step = one full frame of the workload per rank (default --scaling weak:
+a batch of N frames, one per GPU, no data-path collective), or one frame with
+its rows sharded across the N ranks and gathered to rank 0 over RCCL
+(--scaling strong). One process per GPU. N=1 workload = config C3 (3840x2160,
+depth 6, cylinder + cube + sphere-for-cone, 4 lights).
 
 Rays = primary + secondary + shadow, counted on the device with the same rule
 as the CPU oracle (include/rt_abi.h rt_stats). value = rays of all ranks per
@@ -38,7 +40,11 @@ def parse():
     p.add_argument("--height", type=int, default=None)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=8)
-    p.add_argument("--shard", choices=["interleaved", "bands"], default="interleaved")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                   help="weak: every rank renders its own full frame (no collective); "
+                        "strong: one frame's rows sharded over the ranks + gather")
+    p.add_argument("--shard", choices=["interleaved", "bands"], default="interleaved",
+                   help="row partition for --scaling strong")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -109,7 +115,8 @@ def main():
     ctx = pkg.RenderContext(local, specialize=args.specialize == "on")
     ctx.set_scene(packed)
     spec_active, spec_ms = ctx.specialized()
-    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=args.shard)
+    mode = "frame" if args.scaling == "weak" else args.shard
+    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=mode)
 
     def barrier():
         if world > 1:
@@ -139,16 +146,8 @@ def main():
     rays_local = st.total_rays()
     flops_local = pkg.abi.algorithmic_flops(st, len(rargs.lights))
     kavg = sum(kernel_ms) / len(kernel_ms) if kernel_ms else 0.0
-    vals = torch.tensor([elapsed, float(rays_local), float(flops_local)], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = vals.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = vals.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0].item())
-        rays_total = float(sm[1].item())
-    else:
-        rays_total = float(rays_local)
+    mx, sm = pkg.dist.reduce_max_sum([elapsed, rays_local], device=dev)
+    elapsed, rays_total = mx[0], sm[1]
 
     if rank == 0:
         per_step_rays = rays_total / args.steps
@@ -168,15 +167,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": "%s: %s" % (args.config, pkg.configs.WORKLOADS[args.config]),
                        "width": packed.width, "height": packed.height, "depth": rargs.depth,
                        "lights": len(rargs.lights), "objects": int(packed.scene.num_objects),
-                       "rays_per_frame": int(per_step_rays),
-                       "parallelism": "rows%d-%s" % (world, args.shard),
+                       "rays_per_step": int(per_step_rays),
+                       "parallelism": ("frame-per-gpu%d" % world) if args.scaling == "weak"
+                                      else "rows%d-%s" % (world, args.shard),
                        "kernel": "specialised" if spec_active else "generic",
                        "spec_compile_ms": round(spec_ms, 1)},
             "roofline": {"bound": "valu-fp64", "achieved": round(achieved_tf, 3), "peak": PEAK_FP64_TFLOPS,

@@ -1,8 +1,14 @@
-"""Sharding one frame across GPUs + gather to rank 0 (RCCL over xGMI).
+"""Multi-GPU rendering, one process per GPU.
 
-Pixels are independent and the jitter RNG depends only on (column, 20-row
-strip) (raytracer.go:627-634), so any row partition renders bit-identical
-rows. One process per GPU. Two partitions:
+Weak scaling (bench default, mode "frame"): a batch of frames, one per rank
+(e.g. the frames of an animation or of independent requests); each rank renders
+its whole frame into its own HBM buffer. The units (frames, and within them
+pixels) are independent, so there is no data-path collective at all.
+
+Strong scaling (one frame sharded across GPUs + gather to rank 0, RCCL over
+xGMI): pixels are independent and the jitter RNG depends only on (column,
+20-row strip) (raytracer.go:627-634), so any row partition renders
+bit-identical rows. Two partitions:
 
 - "interleaved" (default): the image's 8-row tile rows are dealt round-robin,
   rank r owning tile rows r, r+N, r+2N, ... -- sky and ground rows are spread
@@ -68,8 +74,25 @@ def gather_frame(buf, height, mode="bands", group=None):
     return None
 
 
+def reduce_max_sum(values, device=None):
+    """(max over ranks, sum over ranks) of a list of floats (one all_reduce
+    each; identity without an initialised process group). Used for the step
+    time (max) and the ray totals (sum)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return t.tolist(), t.tolist()
+    mx, sm = t.clone(), t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return mx.tolist(), sm.tolist()
+
+
 class DistributedRenderer:
-    """Renders one frame per step with rows sharded over the process group."""
+    """Per step: this rank's whole frame (mode "frame", weak scaling), or its
+    share of one frame's rows ("interleaved" / "bands", strong scaling) followed
+    by the gather to rank 0."""
 
     def __init__(self, ctx, packed, rank, world, device, mode="interleaved"):
         import torch
@@ -80,7 +103,9 @@ class DistributedRenderer:
         self.mode = mode
         self.H = packed.height
         self.W = packed.width
-        if mode == "interleaved":
+        if mode == "frame":
+            rows = self.H
+        elif mode == "interleaved":
             self.nt, self.K = tile_rows(self.H, world)
             # this rank's valid tile rows (the rest of its slab is padding)
             self.ntrows = max(0, min(self.K, (self.nt - rank + world - 1) // world))
@@ -91,6 +116,8 @@ class DistributedRenderer:
         self.frame = None
 
     def has_work(self):
+        if self.mode == "frame":
+            return True
         return self.ntrows > 0 if self.mode == "interleaved" else self.y1 > self.y0
 
     def step(self, gather=True, events=None):
@@ -99,6 +126,12 @@ class DistributedRenderer:
         kernel, for kernel timing without a host sync per step."""
         if events is not None:
             events[0].record()
+        if self.mode == "frame":
+            self.ctx.render_rows_async(0, self.H, self.buf)
+            if events is not None:
+                events[1].record()
+            self.frame = self.buf  # rank-local frame; nothing to exchange
+            return self.frame
         if self.mode == "interleaved":
             if self.ntrows > 0:
                 self.ctx.render_tile_rows_async(self.rank, self.world, self.ntrows,

@@ -86,3 +86,63 @@ def test_band_rows_cover_the_frame_once():
                 assert 0 <= y0 <= y1 <= h and y1 - y0 <= per
                 rows.extend(range(y0, y1))
             assert rows == list(range(h))
+
+
+class _OracleCtx:
+    """Stand-in for RenderContext in CPU tests: renders rows with the oracle."""
+
+    def __init__(self, packed, oracle_bind):
+        self.packed, self.ob = packed, oracle_bind
+
+    def render_rows_async(self, y0, y1, out, stream=None):
+        img, _ = self.ob.render_rows(self.packed, y0, y1, threads=2)
+        out[: y1 - y0] = torch.from_numpy(img)
+
+
+def _weak_worker(rank, world, port, w, h, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    import oracle_bind
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    packed = pkg.scene.convert(pkg.configs.c2(width=w, height=h))
+    dr = pkg.dist.DistributedRenderer(_OracleCtx(packed, oracle_bind), packed, rank, world, "cpu", mode="frame")
+    assert dr.has_work()
+    frame = dr.step()  # no collective in this mode
+    mx, sm = pkg.dist.reduce_max_sum([rank + 1.0, 10.0 * (rank + 1)])
+    q.put((rank, frame.numpy().copy(), mx, sm))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_weak_scaling_frame_per_rank():
+    """bench.py default (--scaling weak): every rank renders the whole frame
+    locally; timing is max over ranks, rays summed."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind
+    import go_raytracer_amd as rt
+    world, w, h = 2, 40, 24
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_weak_worker, args=(r, world, port, w, h, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full, _ = oracle_bind.render_rows(rt.scene.convert(rt.configs.c2(width=w, height=h)))
+    for rank, frame, mx, sm in got:
+        assert np.array_equal(frame, full), rank
+        assert mx == [2.0, 20.0] and sm == [3.0, 30.0]
+
+
+def test_reduce_max_sum_without_process_group():
+    import go_raytracer_amd as rt
+    assert rt.dist.reduce_max_sum([1.5, 2.0]) == ([1.5, 2.0], [1.5, 2.0])
