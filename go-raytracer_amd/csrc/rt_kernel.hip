@@ -426,6 +426,7 @@ int align16(int v) { return (v + 15) & ~15; }
 struct rt_context {
   int device = 0;
   int cus = 0;
+  int lds_per_cu = 0, lds_per_block = 0;  // bytes (device properties)
   int grid_lds = 0, grid_glb = 0;  // persistent grids (workgroups) per kernel flavour
   DevScene sc;
   bool has_scene = false;
@@ -568,14 +569,22 @@ struct SpecKey {
   }
 };
 
+// Scene blob staged in LDS (small scenes) or read from global memory with
+// wave-uniform scalar loads. RT_SCENE_GLOBAL=1 forces the global flavour
+// (tuning experiments only).
+bool scene_in_lds(const DevScene& s) {
+  static const bool force_global = getenv("RT_SCENE_GLOBAL") && atoi(getenv("RT_SCENE_GLOBAL")) != 0;
+  return !force_global && s.blob_bytes <= (int)LDS_MAX_BYTES;
+}
+
 // Specialisation of a scene; false when it runs the generic kernel (no
 // objects).
 bool spec_key(const DevScene& s, SpecKey* k) {
   if (s.nobj < 1) return false;
-  k->lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
+  k->lds = scene_in_lds(s);
   k->bvh = s.use_bvh;
   k->csg = s.has_csg;
-  k->nobj = (!s.use_bvh && !s.has_csg && k->lds && s.nobj <= SPEC_MAX_OBJ) ? s.nobj : 0;
+  k->nobj = (!s.use_bvh && !s.has_csg && s.nobj <= SPEC_MAX_OBJ) ? s.nobj : 0;
   k->kinds.clear();
   for (int i = 0; i < k->nobj; i++) k->kinds += (i ? "," : "") + std::to_string(s.kinds[i]);
   k->kmask = s.kind_mask | s.leaf_kind_mask;  // CSG leaves are shaded by their own kind
@@ -743,6 +752,8 @@ int rt_create(int device, rt_context** out) {
     return fail(RT_E_DEVICE, "hipGetDeviceProperties failed");
   }
   c->cus = prop.multiProcessorCount;
+  c->lds_per_cu = (int)prop.maxSharedMemoryPerMultiProcessor;
+  c->lds_per_block = (int)prop.sharedMemPerBlock;
   // Persistent grids: as many workgroups as are resident (any extra block just
   // finds the queue drained). The LDS flavour is sized for the LDS budget.
   int per_cu = 0;
@@ -1227,12 +1238,15 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const DevScene& s = c->sc;
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
-  const bool lds = s.blob_bytes <= (int)LDS_MAX_BYTES;
-  const int frames_off = lds ? s.blob_bytes : 0;
-  const int vm_off = frames_off + WAVES_PER_WG * RT_LDS_FRAMES * CORE * 64 * (int)sizeof(double);
+  const bool lds = scene_in_lds(s);
+  // Dynamic LDS: [scene blob (LDS flavour)] [VM records] [BVH stack]
+  // [counters] [PCG jump table] [frame cores of the first lds_levels levels]
+  const int vm_off = lds ? s.blob_bytes : 0;
   const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
   const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * 12 : 0);
-  const int shmem = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
+  const int jump_off = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
+  const int frames_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);
+  int shmem = frames_off;
   const void* kfn;
   if (s.has_csg)
     kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, true> : (const void*)rt_render_kernel<true, false, true>)
@@ -1241,18 +1255,36 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, false> : (const void*)rt_render_kernel<true, false, false>)
               : (s.use_bvh ? (const void*)rt_render_kernel<false, true, false> : (const void*)rt_render_kernel<false, false, false>);
   hipFunction_t spec = c->spec_fn;  // built for this scene's flavour (spec_key)
-  int per_cu = 0;
-  if (spec) {
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, spec, WG, shmem) != hipSuccess) per_cu = 0;
-  } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, WG, shmem) != hipSuccess) {
-    per_cu = 0;
-  }
+  auto occupancy = [&](int bytes) {
+    int n = 0;
+    if (spec) {
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, spec, WG, bytes) != hipSuccess) n = 0;
+    } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, WG, bytes) != hipSuccess) {
+      n = 0;
+    }
+    return n;
+  };
+  int per_cu = occupancy(shmem);
   if (per_cu <= 0) per_cu = 1;
+  // The frame cores of the shallowest recursion levels live in the LDS that
+  // is left over at this occupancy (never lowering it); deeper levels stay in
+  // the HBM frame stack. RT_LDS_LEVELS=n caps the count (experiments).
+  const int level_bytes = WAVES_PER_WG * CORE * 64 * (int)sizeof(double);
+  int lds_levels = 0;
+  if (c->lds_per_cu > 0 && c->lds_per_block > 0) {
+    const int avail = std::min(c->lds_per_block, c->lds_per_cu / std::min(per_cu, 8)) - shmem;
+    lds_levels = std::max(0, std::min(std::max(1, s.depth - 1), avail / level_bytes));
+    if (const char* e = getenv("RT_LDS_LEVELS")) lds_levels = std::min(lds_levels, std::max(0, atoi(e)));
+    while (lds_levels > 0 && occupancy(shmem + lds_levels * level_bytes) < per_cu) lds_levels--;
+  }
+  shmem += lds_levels * level_bytes;
   const int grid = c->cus * std::min(per_cu, 8);
   if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
   Params P;
   std::memset(&P, 0, sizeof P);
   P.lds_frames_off = frames_off;
+  P.lds_levels = lds_levels;
+  P.jump_off = jump_off;
   P.off_geo = s.off_geo;
   P.off_shade = s.off_shade;
   P.off_mats = s.off_mats;

@@ -34,8 +34,8 @@
 #ifndef RT_CULL
 #define RT_CULL 1  // wave-uniform conservative bounding-sphere culling (exact, see may_hit)
 #endif
-#ifndef RT_LDS_FRAMES
-#define RT_LDS_FRAMES 0  // recursion levels whose frame core lives in LDS (measured: no gain)
+#ifndef RT_STMAX_F32
+#define RT_STMAX_F32 0  // shadow-ray cull bound dist/|d| from an FP32 reciprocal (exact: bound only)
 #endif
 #ifndef RT_CUBE_FAST
 #define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
@@ -93,7 +93,7 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
 // Frame of one traceRay activation that has children (post-order combine).
 // Global layout: 14 fields, lane-interleaved: Lw[3] cfirst[3] pend_o[3]
 // pend_d[3] kr packed. The CORE fields (Lw, kr, packed) of the first
-// RT_LDS_FRAMES levels live in LDS instead; cfirst/pending (only used when a
+// P.lds_levels levels live in LDS instead; cfirst/pending (only used when a
 // material is both reflective and transparent) always live in HBM.
 enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
@@ -107,6 +107,8 @@ enum { LDS_MAX_BYTES = RT_LDS_MAX };
 
 struct Params {
   int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
+  int lds_levels;      // recursion levels whose frame core lives in LDS (host: LDS left at full occupancy)
+  int jump_off;        // byte offset of the LDS copy of the PCG jump table
   int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_csg, off_code, off_consts,
       off_entry, blob_bytes;
   int lds_vm_off;     // LDS byte offset of the per-lane VM material records (LDS flavour)
@@ -815,16 +817,19 @@ template <bool LDS, bool BVH, bool CSG>
 __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char* __restrict__ blob, Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const char* base;
+  // Stage the PCG jump table (and, LDS flavour, the whole scene) once per
+  // workgroup (the only block-wide barrier).
+  uint64_t* jtab = reinterpret_cast<uint64_t*>(smem + P.jump_off);
+  if (threadIdx.x < 20 * 4) jtab[threadIdx.x] = P.jump[threadIdx.x];
   if constexpr (LDS) {
-    // Stage the whole scene once per workgroup (the only block-wide barrier).
     const int n16 = P.blob_bytes / 16;
     for (int i = threadIdx.x; i < n16; i += WG)
       reinterpret_cast<uint4*>(smem)[i] = reinterpret_cast<const uint4*>(blob)[i];
-    __syncthreads();
     base = smem;
   } else {
     base = blob;
   }
+  __syncthreads();
   View S;
   S.geo = reinterpret_cast<const double*>(base + P.off_geo);
   S.shade = reinterpret_cast<const double*>(base + P.off_shade);
@@ -843,15 +848,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   const int lane = (int)(threadIdx.x & 63);
   const int wslot = (int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
   double* stk = P.stack + (size_t)wslot * ((size_t)P.frames * FRAME_FIELDS * 64) + lane;
+  const int lds_lv = P.lds_levels;
   double* lfr = reinterpret_cast<double*>(smem + P.lds_frames_off) +
-                (size_t)(threadIdx.x >> 6) * (RT_LDS_FRAMES * CORE * 64) + lane;
-  // frame core accessors: level < RT_LDS_FRAMES in LDS, deeper in HBM
+                (size_t)(threadIdx.x >> 6) * (lds_lv * CORE * 64) + lane;
+  // frame core accessors: level < lds_levels in LDS, deeper in HBM
   auto core_ld = [&](int level, int c) -> double {
-    if (level < RT_LDS_FRAMES) return lfr[(level * CORE + c) * 64];
+    if (level < lds_lv) return lfr[(level * CORE + c) * 64];
     return frame_ptr(stk, level)[core_gfield(c) * 64];
   };
   auto core_st = [&](int level, int c, double v) {
-    if (level < RT_LDS_FRAMES)
+    if (level < lds_lv)
       lfr[(level * CORE + c) * 64] = v;
     else
       frame_ptr(stk, level)[core_gfield(c) * 64] = v;
@@ -1024,7 +1030,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           // (raytracer.go:632-643: 2 draws per sample, 4 samples per row).
           int ymin = y - y % 20;
           Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
-          const uint64_t* j = P.jump + (size_t)(y % 20) * 4;
+          const uint64_t* j = jtab + (y % 20) * 4;
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sample = 0;
           sum = mk(0, 0, 0);
@@ -1271,6 +1277,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     d3 L = mk(0, 0, 0);
     if (hit) L = scale(mk(G[0], G[1], G[2]), M[9]);
     const double rlen = len(ray.d);
+#if RT_STMAX_F32
+    const float rlen_rcpf = __builtin_amdgcn_rcpf((float)rlen);
+#endif
     const d3 sorig = add(pw, scale(nw, 1e-4));
     uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind (cones: below)
     for (int li = 0; li < P.nlights; li++) {
@@ -1293,7 +1302,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       const F3 sof = f3(sorig), sdf = f3(ldir);
       const float sslack = ray_slack(sof);
       // occluders must lie within t < dist / |ray.d| (raytracer.go:424)
+#if RT_STMAX_F32
+      // FP32 reciprocal instead of an FP64 division: relative error < 4 ulp(f32)
+      // ~ 2.4e-7, far inside the 1e-4 margin (NaN / inf cases as in FP64;
+      // dist = 0 culls everything, and nothing can occlude within t*|d| < 0)
+      const float stmax = (float)dist * rlen_rcpf * 1.0001f + 1e-4f;
+#else
       const float stmax = (float)(dist / rlen) * 1.0001f + 1e-4f;
+#endif
       // inShadow's test count is #{i < end, i != hit} with end = first
       // occluder + 1 (or nobj); counted per kind from the prefix table below.
       int send = P.nobj;
