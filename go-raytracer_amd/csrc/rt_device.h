@@ -198,7 +198,30 @@ __device__ __noinline__ double go_pow_general(double x, double y) {
 // Ldexp loop below (same ops, same order); x == 0 takes its zero case. The
 // general routine (with the exp/log fraction path) stays out of line: inlined
 // it doubled the kernel's register spills.
+#ifndef RT_POW_DIRECT
+#define RT_POW_DIRECT 1  // exact direct binary powering for small integer exponents (see go_pow)
+#endif
 __device__ __forceinline__ double go_pow(double x, double y) {
+#if RT_POW_DIRECT
+  // Integer 2 <= y <= 64 and 2^-15 <= x <= 2^15: every power the loop below
+  // forms (x^(2^k) for 2^k <= y, and the partial products, all between x^y and
+  // 1) is a normal number, where round-to-nearest commutes with scaling by
+  // powers of two. Go's mantissa renormalisation (x1 += x1, xe--) and the final
+  // Ldexp therefore only move exponents: the same multiplications on x itself
+  // round identically, and the result is a1 (its xe guard cannot trigger:
+  // |xe| <= 16 * 64). The square after the last bit is unused in Go, so it is
+  // skipped here (it could leave the normal range).
+  if (x >= 0x1p-15 && x <= 0x1p15 && y >= 2 && y <= 64 && __builtin_floor(y) == y) {
+    double a1 = 1.0, x1 = x;
+    for (int i = (int)y;;) {
+      if (i & 1) a1 *= x1;
+      i >>= 1;
+      if (i == 0) break;
+      x1 *= x1;
+    }
+    return a1;
+  }
+#endif
   if (x > 0 && x < __builtin_inf() && x != 1 && y >= 2 && y < 2147483648.0 && __builtin_floor(y) == y) {
     int xe;
     double x1 = frexp(x, &xe);
