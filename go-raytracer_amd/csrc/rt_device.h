@@ -45,19 +45,24 @@ __device__ __forceinline__ double rcp_refined(double d) {
   e = __builtin_fma(-d, y, 1.0);
   return __builtin_fma(y, e, y);
 }
+// A zero residual means q is the exact quotient: return it as is, which also
+// keeps the sign of a zero numerator (div_fmas would give +0 for n = -0, and
+// div_fixup restores the sign), so zero numerators need no fallback.
 __device__ __forceinline__ double div_rcp(double n, double d, double y) {
   const double q = n * y;
-  return __builtin_fma(__builtin_fma(-d, q, n), y, q);
+  const double e = __builtin_fma(-d, q, n);
+  return e == 0.0 ? q : __builtin_fma(e, y, q);
 }
+__device__ __forceinline__ bool num_safe(double n) { return n == 0.0 || div_safe(n); }
 #ifndef RT_SHARED_DIV
-#define RT_SHARED_DIV 0  // measured neutral on C2/C3/C4 (code size vs. saved FP64 ops)
+#define RT_SHARED_DIV 0  // measured slower on C3 (4.74 vs 4.56 ms): code size and selects outweigh the saved FP64 ops
 #endif
 __device__ __forceinline__ d3 norm(d3 v) {                                                        // vec.go:78
   double m = __builtin_sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
 #if RT_SHARED_DIV
   const double y = rcp_refined(m);
   d3 r = mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
-  const bool ok = div_safe(m) && div_safe(v.x) && div_safe(v.y) && div_safe(v.z);
+  const bool ok = div_safe(m) && num_safe(v.x) && num_safe(v.y) && num_safe(v.z);
   if (__any(!ok)) {
     if (!ok) r = mk(v.x / m, v.y / m, v.z / m);
   }
