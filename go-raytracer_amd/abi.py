@@ -20,6 +20,11 @@ KIND_NAMES = ("sphere", "plane", "cube", "cylinder", "cone", "csg")
 RT_CSG_UNION, RT_CSG_INTERSECT, RT_CSG_DIFFERENCE = -1, -2, -3
 RT_CSG_MAX_LEAVES = 128
 RT_SPEC_SURFACES, RT_SPEC_DIRECTIONAL, RT_SPEC_SPOT = 1, 2, 4  # rt_spec_precompile feature bits
+
+
+def RT_SPEC_LIGHTS(n):
+    """rt_spec_precompile feature bits for exactly n (1..8) lights (include/rt_abi.h)."""
+    return int(n) << 8
 RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_SPOT = 0, 1, 2
 
 

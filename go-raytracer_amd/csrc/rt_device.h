@@ -254,6 +254,28 @@ __device__ __forceinline__ double go_pow(double x, double y) {
   return go_pow_general(x, y);
 }
 
+// go_pow's direct path without branches, for interleaving several powers:
+// ok reports whether (x, y) is in that path's domain (then the result equals
+// go_pow(x, y) bit for bit), extended to x = +0, where every power is +0 as
+// in Go's Pow(+0, y > 0). Squares past the exponent's top bit may leave the
+// normal range; they are never multiplied in. RT_SPEC_POWBITS (host: bit
+// length of the scene's largest integer exponent) bounds the unrolled steps.
+#ifndef RT_SPEC_POWBITS
+#define RT_SPEC_POWBITS 7
+#endif
+__device__ __forceinline__ double pow_small_int(double x, double y, bool& ok) {
+  ok = (x == 0.0 || (x >= 0x1p-15 && x <= 0x1p15)) && y >= 2 && y <= (double)((1 << RT_SPEC_POWBITS) - 1) &&
+       y <= 64 && __builtin_floor(y) == y && !signbit64(x);
+  const int n = ok ? (int)y : 0;
+  double a1 = 1.0, x1 = x;
+#pragma unroll
+  for (int k = 0; k < RT_SPEC_POWBITS; k++) {
+    if ((n >> k) & 1) a1 = a1 * x1;
+    if (k + 1 < RT_SPEC_POWBITS) x1 = x1 * x1;
+  }
+  return a1;
+}
+
 // math/rand/v2 PCG (pcg.go): 128-bit LCG, DXSM output; Rand.Float64.
 struct Pcg {
   uint64_t hi, lo;

@@ -223,6 +223,7 @@ bool go_tan(double x, double& out) {
 
 struct DevScene {
   int width = 0, height = 0, depth = 0, nobj = 0, nlights = 0, nmats = 0;
+  int pow_bits = 7;  // bit length of the largest integer specular exponent in 2..64 (7 with surface programs)
   double vw = 0, vh = 0;
   double amb[3] = {0, 0, 0}, bg0[3] = {0, 0, 0}, bg1[3] = {0, 0, 0};
   char* blob = nullptr;
@@ -490,7 +491,7 @@ int upload(T** dst, const std::vector<T>& src) {
 // Compiled code objects are cached per process by specialisation key, loaded
 // modules per (device, key).
 // ---------------------------------------------------------------------------
-enum { SPEC_MAX_OBJ = 8 };
+enum { SPEC_MAX_OBJ = 8, SPEC_MAX_LIGHTS = 8 };
 static_assert(SF_VM == RT_SPEC_SURFACES && SF_LDIR == RT_SPEC_DIRECTIONAL && SF_LSPOT == RT_SPEC_SPOT,
               "feature bits of rt_render.h and include/rt_abi.h");
 
@@ -562,10 +563,11 @@ bool rtc_load() {
 struct SpecKey {
   int lds = 1, bvh = 0, csg = 0, nobj = 0;
   std::string kinds;
-  int kmask = 0, feat = 0;
+  int kmask = 0, feat = 0, nlights = 0;  // nlights > 0: light loop unrolled for that count
+  int pow_bits = 7;                      // unrolled specular powering steps
   std::string str() const {
     return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
-           std::to_string(kmask) + ":" + std::to_string(feat);
+           std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits);
   }
 };
 
@@ -590,6 +592,8 @@ bool spec_key(const DevScene& s, SpecKey* k) {
   k->kmask = s.kind_mask | s.leaf_kind_mask;  // CSG leaves are shaded by their own kind
   k->feat = (s.num_programs ? SF_VM : 0) | ((s.light_mask >> RT_LIGHT_DIRECTIONAL) & 1 ? SF_LDIR : 0) |
             ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
+  k->nlights = (s.nlights >= 1 && s.nlights <= SPEC_MAX_LIGHTS) ? s.nlights : 0;
+  k->pow_bits = s.num_programs ? 7 : s.pow_bits;  // surface programs set exponents at run time
   return true;
 }
 
@@ -607,6 +611,8 @@ int spec_compile(const SpecKey& sk, double* ms) {
     defs.push_back("-DRT_SPEC_NOBJ=" + std::to_string(sk.nobj));
     defs.push_back("-DRT_SPEC_KINDS=" + sk.kinds);
   }
+  if (sk.nlights > 0) defs.push_back("-DRT_SPEC_NLIGHTS=" + std::to_string(sk.nlights));
+  defs.push_back("-DRT_SPEC_POWBITS=" + std::to_string(sk.pow_bits));
   std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
   for (const auto& d : defs) opts.push_back(d.c_str());
   // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only)
@@ -709,7 +715,9 @@ int rt_set_specialize(rt_context* c, int enable) {
 
 int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile_ms) {
   if (compile_ms) *compile_ms = 0;
-  if (features & ~(SF_VM | SF_LDIR | SF_LSPOT)) return fail(RT_E_INVALID, "rt_spec_precompile: unknown feature bits");
+  if (features & ~(SF_VM | SF_LDIR | SF_LSPOT | (0xF << 8))) return fail(RT_E_INVALID, "rt_spec_precompile: unknown feature bits");
+  const int nlights = (features >> 8) & 0xF;
+  if (nlights > SPEC_MAX_LIGHTS) return fail(RT_E_INVALID, "rt_spec_precompile: 0..8 lights");
   if (nobj < 1 || nobj > SPEC_MAX_OBJ || !kinds) return fail(RT_E_INVALID, "rt_spec_precompile: 1..8 objects");
   SpecKey sk;
   sk.nobj = nobj;
@@ -719,7 +727,8 @@ int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile
     sk.kinds += (i ? "," : "") + std::to_string(kinds[i]);
     sk.kmask |= 1 << kinds[i];
   }
-  sk.feat = features;
+  sk.feat = features & (SF_VM | SF_LDIR | SF_LSPOT);
+  sk.nlights = nlights;
   std::lock_guard<std::mutex> lock(g_spec_mu);
   double ms = 0;
   int rc = spec_compile(sk, &ms);
@@ -1045,6 +1054,16 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     d[10] = mm.ks;
     d[11] = mm.specular_exponent;
   }
+  {  // unrolled steps of the device's branch-free specular powering (pow_small_int)
+    int maxn = 1;
+    for (int m = 0; m < s.nmats; m++) {
+      const double n = in->materials[m].specular_exponent;
+      if (n >= 2 && n <= 64 && std::floor(n) == n) maxn = std::max(maxn, (int)n);
+    }
+    int bits = 0;
+    while ((1 << bits) <= maxn) bits++;
+    s.pow_bits = std::max(1, bits);
+  }
   std::vector<double> lights(GLOB + (size_t)std::max(1, s.nlights) * LGT, 0.0);
   for (int k = 0; k < 3; k++) {
     lights[k] = s.amb[k];
@@ -1269,21 +1288,33 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // The frame cores of the shallowest recursion levels live in the LDS that
   // is left over at this occupancy (never lowering it); deeper levels stay in
   // the HBM frame stack. RT_LDS_LEVELS=n caps the count (experiments).
+  // RT_LDS_FULL=n (experiments) also moves the other frame fields (first
+  // child's colour, pending refraction ray) of the first n levels to LDS.
   const int level_bytes = WAVES_PER_WG * CORE * 64 * (int)sizeof(double);
-  int lds_levels = 0;
+  const int ext_bytes = WAVES_PER_WG * 9 * 64 * (int)sizeof(double);
+  const int frames = std::max(1, s.depth - 1);
+  int lds_levels = 0, lds_full = 0;
   if (c->lds_per_cu > 0 && c->lds_per_block > 0) {
     const int avail = std::min(c->lds_per_block, c->lds_per_cu / std::min(per_cu, 8)) - shmem;
-    lds_levels = std::max(0, std::min(std::max(1, s.depth - 1), avail / level_bytes));
-    if (const char* e = getenv("RT_LDS_LEVELS")) lds_levels = std::min(lds_levels, std::max(0, atoi(e)));
-    while (lds_levels > 0 && occupancy(shmem + lds_levels * level_bytes) < per_cu) lds_levels--;
+    if (const char* e = getenv("RT_LDS_FULL")) lds_full = std::max(0, std::min(frames, atoi(e)));
+    while (lds_full > 0 && lds_full * (ext_bytes + level_bytes) > avail) lds_full--;
+    lds_levels = std::max(lds_full, std::min(frames, (avail - lds_full * ext_bytes) / level_bytes));
+    if (const char* e = getenv("RT_LDS_LEVELS")) lds_levels = std::max(lds_full, std::min(lds_levels, atoi(e)));
+    while (lds_levels > 0 && occupancy(shmem + lds_levels * level_bytes + lds_full * ext_bytes) < per_cu) {
+      lds_levels--;
+      lds_full = std::min(lds_full, lds_levels);
+    }
   }
-  shmem += lds_levels * level_bytes;
+  const int ext_off = shmem + lds_levels * level_bytes;
+  shmem = ext_off + lds_full * ext_bytes;
   const int grid = c->cus * std::min(per_cu, 8);
   if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
   Params P;
   std::memset(&P, 0, sizeof P);
   P.lds_frames_off = frames_off;
   P.lds_levels = lds_levels;
+  P.lds_full = lds_full;
+  P.lds_ext_off = ext_off;
   P.jump_off = jump_off;
   P.off_geo = s.off_geo;
   P.off_shade = s.off_shade;
@@ -1420,6 +1451,13 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
                         "leaves/traversal trace=%.1f shadow=%.1f\n", bd[4], bd[5], (double)bd[0] / (double)std::max(1ull, bd[4]),
                 (double)bd[1] / (double)std::max(1ull, bd[5]), (double)bd[2] / (double)std::max(1ull, bd[4]),
                 (double)bd[3] / (double)std::max(1ull, bd[5]));
+#ifdef RT_EXACT_DIAG
+      unsigned long long ex[2 * RT_NUM_KINDS + 2];
+      HIP_TRY(hipMemcpy(ex, c->stats + ST_EXDIAG, sizeof ex, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[exact] lane tests after culling per kind (trace/shadow):");
+      for (int k = 0; k < RT_NUM_KINDS; k++) fprintf(stderr, " k%d=%llu/%llu", k, ex[2 * k], ex[2 * k + 1]);
+      fprintf(stderr, "; wave batches trace=%llu shadow=%llu\n", ex[2 * RT_NUM_KINDS], ex[2 * RT_NUM_KINDS + 1]);
+#endif
     }
   }
 #endif

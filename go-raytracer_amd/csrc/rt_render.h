@@ -98,7 +98,7 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
 enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
-       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24 };
+       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32 };  // (stats buffer: 64 entries)
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
 #ifndef RT_LDS_MAX
 #define RT_LDS_MAX (40 * 1024)
@@ -108,6 +108,8 @@ enum { LDS_MAX_BYTES = RT_LDS_MAX };
 struct Params {
   int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
   int lds_levels;      // recursion levels whose frame core lives in LDS (host: LDS left at full occupancy)
+  int lds_full;        // recursion levels whose other frame fields (3..11) live in LDS too
+  int lds_ext_off;     // byte offset of those fields in dynamic LDS
   int jump_off;        // byte offset of the LDS copy of the PCG jump table
   int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_csg, off_code, off_consts,
       off_entry, blob_bytes;
@@ -372,12 +374,13 @@ __device__ __forceinline__ F3 f3(d3 v) { return F3{(float)v.x, (float)v.y, (floa
 // ray origin, so origins far from the object stay conservative.
 __device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g, float slack) {
   const float* b = reinterpret_cast<const float*>(g + 12);
+  // (fused multiply-adds: only less rounding than the bound allows for)
   float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
-  float tc = ox * d.x + oy * d.y + oz * d.z;
+  float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
   tc = fminf(fmaxf(tc, 0.0f), tmax);
-  float qx = ox - tc * d.x, qy = oy - tc * d.y, qz = oz - tc * d.z;
+  float qx = __builtin_fmaf(-tc, d.x, ox), qy = __builtin_fmaf(-tc, d.y, oy), qz = __builtin_fmaf(-tc, d.z, oz);
   const float R = b[3] + slack;
-  return qx * qx + qy * qy + qz * qz <= R * R;
+  return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= R * R;
 }
 __device__ __forceinline__ float ray_slack(F3 o) {
   return 1e-5f * (1.0f + __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z));
@@ -626,18 +629,19 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
 // bound: then f(0) and the slope must agree in sign (the root lies behind).
 __device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, const double* sh) {
   const float* c = reinterpret_cast<const float*>(sh + 16);
-  const float f0 = c[0] * o.x + c[1] * o.y + c[2] * o.z + c[3];
-  const float sl = c[0] * d.x + c[1] * d.y + c[2] * d.z;
-  const float a0 = c[4] * __builtin_fabsf(o.x) + c[5] * __builtin_fabsf(o.y) + c[6] * __builtin_fabsf(o.z) + c[7];
-  const float a1 = c[4] * __builtin_fabsf(d.x) + c[5] * __builtin_fabsf(d.y) + c[6] * __builtin_fabsf(d.z);
+  const float f0 = __builtin_fmaf(c[0], o.x, __builtin_fmaf(c[1], o.y, __builtin_fmaf(c[2], o.z, c[3])));
+  const float sl = __builtin_fmaf(c[0], d.x, __builtin_fmaf(c[1], d.y, c[2] * d.z));
+  const float a0 = __builtin_fmaf(c[4], __builtin_fabsf(o.x),
+                                  __builtin_fmaf(c[5], __builtin_fabsf(o.y), __builtin_fmaf(c[6], __builtin_fabsf(o.z), c[7])));
+  const float a1 = __builtin_fmaf(c[4], __builtin_fabsf(d.x), __builtin_fmaf(c[5], __builtin_fabsf(d.y), c[6] * __builtin_fabsf(d.z)));
   float f1, m0, m1;
   if (tmax >= 1e30f) {
     f1 = sl;
-    m0 = 1e-4f * a0 + 1e-30f;
-    m1 = 1e-4f * a1 + 1e-30f;
+    m0 = __builtin_fmaf(1e-4f, a0, 1e-30f);
+    m1 = __builtin_fmaf(1e-4f, a1, 1e-30f);
   } else {
-    f1 = f0 + tmax * sl;
-    m0 = 1e-4f * (a0 + tmax * a1) + 1e-30f;
+    f1 = __builtin_fmaf(tmax, sl, f0);
+    m0 = __builtin_fmaf(1e-4f, __builtin_fmaf(tmax, a1, a0), 1e-30f);
     m1 = m0;
   }
   return !((f0 > m0 && f1 > m1) || (f0 < -m0 && f1 < -m1));
@@ -663,6 +667,22 @@ __device__ __forceinline__ uint64_t stamp() {
 #else
 #define PH_BEGIN() (void)0
 #define PH_MARK(k) (void)0
+#endif
+
+// Diagnostic build: lanes reaching an exact FP64 Intersect after culling,
+// per kind and loop (trace 0 / shadow 1), and wave batches per loop
+// (global atomics: build with RT_EXACT_DIAG only when phase times don't matter).
+#ifdef RT_EXACT_DIAG
+#define EXDIAG(k, sh, b)                                                                    \
+  do {                                                                                      \
+    const uint64_t act_ = __ballot(1), m_ = __ballot(b);                                    \
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1) {                          \
+      atomicAdd(P.stats + ST_EXDIAG + 2 * (k) + (sh), (unsigned long long)__popcll(m_));    \
+      atomicAdd(P.stats + ST_EXDIAG + 2 * RT_NUM_KINDS + (sh), 1ull);                       \
+    }                                                                                       \
+  } while (0)
+#else
+#define EXDIAG(k, sh, b) (void)0
 #endif
 
 // Frame stack: lane-interleaved so that one field of one frame is a
@@ -856,6 +876,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (level < lds_lv) return lfr[(level * CORE + c) * 64];
     return frame_ptr(stk, level)[core_gfield(c) * 64];
   };
+  // Frame fields 3..11 (first child's colour, pending refraction ray) of
+  // `level`: row j - 3 of the returned pointer (LDS for level < lds_full).
+  const int lds_full = P.lds_full;
+  double* lext = reinterpret_cast<double*>(smem + P.lds_ext_off) + (size_t)(threadIdx.x >> 6) * (lds_full * 9 * 64) + lane;
+  auto ext = [&](int level) -> double* {
+    return level < lds_full ? lext + (size_t)level * 9 * 64 : frame_ptr(stk, level) + 3 * 64;
+  };
   auto core_st = [&](int level, int c, double v) {
     if (level < lds_lv)
       lfr[(level * CORE + c) * 64] = v;
@@ -950,17 +977,17 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           int fl = (int)(packed & 0xff);
           if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
             // reflection child done; trace the pending refraction child
-            st3(f, 3, res);
+            st3(ext(sp - 1), 0, res);
             core_st(sp - 1, 4, __longlong_as_double(packed | FL_STAGE));
-            ray.o = ld3(f, 6);
-            ray.d = ld3(f, 9);
+            ray.o = ld3(ext(sp - 1), 3);
+            ray.d = ld3(ext(sp - 1), 6);
             state = S_TRACE;
             have_res = false;
           } else {
             const double* FM = S.mats + (size_t)(packed >> 8) * MAT;
             d3 R = mk(0, 0, 0), Tr = mk(0, 0, 0);
             if ((fl & FL_HASR) && (fl & FL_HAST)) {
-              R = ld3(f, 3);
+              R = ld3(ext(sp - 1), 0);
               Tr = res;
             } else if (fl & FL_HASR) {
               R = res;
@@ -1086,6 +1113,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                                       : may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
         if (!__any(test)) return;
 #endif
+        EXDIAG(k, 0, test);
         if (test) {
           double t;
           int f;
@@ -1282,12 +1310,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #endif
     const d3 sorig = add(pw, scale(nw, 1e-4));
     uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind (cones: below)
-    for (int li = 0; li < P.nlights; li++) {
-      const double* lt = S.lights + (size_t)li * LGT;
-      const int lkind = (int)lt[9];  // wave-uniform
-      d3 ldir;
-      double dist;
-      if (spec_feat(SF_LDIR) && lkind == RT_LIGHT_DIRECTIONAL) {  // extension: light at infinity
+    // Direction and distance to a light (raytracer.go:378-380).
+    auto light_dir = [&](const double* lt, d3& ldir, double& dist) {
+      if (spec_feat(SF_LDIR) && (int)lt[9] == RT_LIGHT_DIRECTIONAL) {  // extension: light at infinity
         ldir = mk(lt[6], lt[7], lt[8]);
         dist = __builtin_inf();
       } else {
@@ -1295,6 +1320,32 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         dist = len(lth);
         ldir = norm(lth);
       }
+    };
+#ifndef RT_LIGHT_SPLIT
+#define RT_LIGHT_SPLIT 0  // lighting after all shadow verdicts (measured: +2.4% VALU instructions)
+#endif
+#ifdef RT_SPEC_NLIGHTS
+    // Specialised: every light's direction up front -- independent sqrt and
+    // division chains the scheduler interleaves -- and the light loop unrolled.
+    d3 ldir_a[RT_SPEC_NLIGHTS];
+    double dist_a[RT_SPEC_NLIGHTS];
+    bool open_a[RT_SPEC_NLIGHTS];
+#pragma unroll
+    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(S.lights + (size_t)li * LGT, ldir_a[li], dist_a[li]);
+#pragma unroll
+    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+      const double* lt = S.lights + (size_t)li * LGT;
+      const int lkind = (int)lt[9];  // wave-uniform
+      const d3 ldir = ldir_a[li];
+      const double dist = dist_a[li];
+#else
+    for (int li = 0; li < P.nlights; li++) {
+      const double* lt = S.lights + (size_t)li * LGT;
+      const int lkind = (int)lt[9];  // wave-uniform
+      d3 ldir;
+      double dist;
+      light_dir(lt, ldir, dist);
+#endif
       bool open = hit;  // lanes still looking for an occluder
       Ray sr;
       sr.o = sorig;
@@ -1331,6 +1382,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                                         : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
           if (!__any(test)) continue;
 #endif
+          EXDIAG(k, 1, test);
           if (test) {
             double t;
             int f;
@@ -1360,6 +1412,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
                                         : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
           if (!__any(test)) return;
+          EXDIAG(k, 1, test);
           if (test) {
             double t;
             int f;
@@ -1447,6 +1500,40 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if (spec_kind(5) && (P.kind_mask & 32)) cnt_add(CNT_ST0 + 5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
       }
       PH_MARK(4);
+#if defined(RT_SPEC_NLIGHTS) && RT_LIGHT_SPLIT
+      open_a[li] = hit && open;
+      (void)lkind;
+    }
+    // Lighting once every shadow verdict is known: the lights' half vectors
+    // and specular powers are independent chains, formed for every lane, and
+    // the terms are added in light order only where the light is visible
+    // (identical arithmetic to the per-light loop below).
+    double ndl_a[RT_SPEC_NLIGHTS], spec_a[RT_SPEC_NLIGHTS], pow_a[RT_SPEC_NLIGHTS];
+    bool pok_a[RT_SPEC_NLIGHTS];
+#pragma unroll
+    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+      ndl_a[li] = go_max0(dot(nw, ldir_a[li]));
+      const d3 H = norm(add(neg(ray.d), ldir_a[li]));
+      spec_a[li] = go_max0(dot(nw, H));
+      pow_a[li] = pow_small_int(spec_a[li], M[11], pok_a[li]);
+    }
+#pragma unroll
+    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+      const double* lt = S.lights + (size_t)li * LGT;
+      if (open_a[li]) {
+        d3 lcol = mk(lt[3], lt[4], lt[5]);
+        if (spec_feat(SF_LSPOT) && (int)lt[9] == RT_LIGHT_SPOT) {  // extension: cone falloff
+          const double ca = dot(neg(ldir_a[li]), mk(lt[6], lt[7], lt[8]));
+          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11]) : 0.0);
+        }
+        d3 diffuse = scale(lcol, ndl_a[li] * M[9]);
+        const double pw_s = pok_a[li] ? pow_a[li] : go_pow(spec_a[li], M[11]);
+        d3 specular = scale(lcol, M[10] * pw_s);
+        L = add(add(L, diffuse), specular);
+      }
+    }
+    PH_MARK(5);
+#else
       if (hit && open) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
         if (spec_feat(SF_LSPOT) && lkind == RT_LIGHT_SPOT) {  // extension: cone falloff
@@ -1462,6 +1549,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       }
       PH_MARK(5);
     }
+#endif
     if (hit) {
       if (spec_kind(0) && (P.kind_mask & 1)) cnt_add(CNT_ST0 + 0, sc0);
       if (spec_kind(1) && (P.kind_mask & 2)) cnt_add(CNT_ST0 + 1, sc1);
@@ -1531,9 +1619,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           core_st(sp, 1, lw.y);
           core_st(sp, 2, lw.z);
           if (hasR && hasT) {
-            double* f = frame_ptr(stk, sp);
-            st3(f, 6, trr.o);
-            st3(f, 9, trr.d);
+            st3(ext(sp), 3, trr.o);
+            st3(ext(sp), 6, trr.d);
           }
           core_st(sp, 3, kr);
           if (spec_feat(SF_VM) && mat < 0) {  // the VM record is per lane: keep what the combine needs

@@ -215,12 +215,14 @@ class RenderContext:
         return out.cpu().numpy()
 
 
-def spec_precompile(kinds, features=0):
+def spec_precompile(kinds, features=0, nlights=0):
     """Compile (no device needed) the specialised kernel for a scene whose
-    objects have these primitive kinds, in order, and RT_SPEC_* feature bits
-    (abi.RT_SPEC_SURFACES / _DIRECTIONAL / _SPOT); returns the compile time
-    (ms, 0 if already cached in this process)."""
+    objects have these primitive kinds, in order, RT_SPEC_* feature bits
+    (abi.RT_SPEC_SURFACES / _DIRECTIONAL / _SPOT) and light count (1..8; the
+    scene's own count, which rt_set_scene specialises on); returns the compile
+    time (ms, 0 if already cached in this process)."""
     lib = load_library()
+    features = int(features) | (int(nlights) << 8)
     arr = (C.c_int * len(kinds))(*[int(k) for k in kinds])
     ms = C.c_double()
     _check(lib.rt_spec_precompile(len(kinds), arr, int(features), C.byref(ms)), "rt_spec_precompile")

@@ -270,6 +270,8 @@ int rt_specialized(rt_context *ctx, int *active, double *compile_ms);
 #define RT_SPEC_SURFACES 1    /* the scene has closure (surface program) materials */
 #define RT_SPEC_DIRECTIONAL 2 /* ... directional lights */
 #define RT_SPEC_SPOT 4        /* ... spot lights */
+#define RT_SPEC_LIGHTS(n) ((n) << 8) /* ... exactly n (1..8) lights, as every scene with 1..8
+                                        lights is specialised (0: the generic light loop) */
 int rt_spec_precompile(int nobj, const int *kinds, int features, double *compile_ms);
 
 /* Diagnostic (tests): run surface program `program` of the context's scene on

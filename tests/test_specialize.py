@@ -13,7 +13,9 @@ A = rt.abi
     ([A.RT_SPHERE, A.RT_CUBE, A.RT_CYLINDER, A.RT_PLANE], 0),  # C2/C3 shape
     ([A.RT_CONE, A.RT_SPHERE], A.RT_SPEC_DIRECTIONAL | A.RT_SPEC_SPOT),
     ([A.RT_CUBE], A.RT_SPEC_SURFACES),
-    ([A.RT_PLANE] * 8, 7)])
+    ([A.RT_PLANE] * 8, 7),
+    ([A.RT_SPHERE, A.RT_CUBE, A.RT_CYLINDER, A.RT_PLANE], A.RT_SPEC_LIGHTS(4)),  # C3 as rt_set_scene keys it
+    ([A.RT_CONE, A.RT_SPHERE], A.RT_SPEC_DIRECTIONAL | A.RT_SPEC_SPOT | A.RT_SPEC_LIGHTS(3))])
 def test_precompile_builds_a_code_object(kinds, feat):
     ms = rt.spec_precompile(kinds, feat)
     assert ms >= 0
@@ -29,3 +31,5 @@ def test_precompile_rejects_bad_requests(kinds):
 def test_precompile_rejects_unknown_feature_bits():
     with pytest.raises(rt.render.RenderError):
         rt.spec_precompile([A.RT_SPHERE], 8)
+    with pytest.raises(rt.render.RenderError):
+        rt.spec_precompile([A.RT_SPHERE], A.RT_SPEC_LIGHTS(9))  # 1..8 lights
