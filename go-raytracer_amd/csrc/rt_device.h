@@ -24,20 +24,56 @@ __device__ __forceinline__ d3 sub(d3 a, d3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ d3 mul(d3 a, d3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }    // vec.go:40
 __device__ __forceinline__ double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }   // vec.go:48
 __device__ __forceinline__ d3 scale(d3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }    // vec.go:70
-__device__ __forceinline__ double len(d3 v) { return __builtin_sqrt(v.x * v.x + v.y * v.y + v.z * v.z); }  // vec.go:95
+// math.Sqrt (correctly rounded). hipcc expands an FP64 sqrt on gfx950 to
+//   scale = x < 2^-767; x' = ldexp(x, scale ? 256 : 0); y = rsq(x');
+//   g = x'y; h = y/2; r = fma(-h, g, 1/2); g = fma(g, r, g); h = fma(h, r, h);
+//   2x { d = fma(-g, g, x'); g = fma(d, h, g) };  g = ldexp(g, scale ? -128 : 0);
+//   result = class(x', +-0 | +inf) ? x' : g
+// For 2^-767 <= x < inf the scaling steps are the identity and the class
+// test is false, so the core below gives the same bits in 10 instead of 18
+// VALU instructions; a wave takes it when all its lanes qualify.
+#ifndef RT_FAST_SQRT
+#define RT_FAST_SQRT 0  // measured: fewer VALU but more scalar branch work, no faster
+#endif
+__device__ __forceinline__ double sqrt_core(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+// True when c holds on every active lane (compare mask == exec: no VALU
+// beyond the compares).
+__device__ __forceinline__ bool wave_all(bool c) {
+  return __builtin_amdgcn_ballot_w64(c) == __builtin_amdgcn_read_exec();
+}
+__device__ __forceinline__ double gsqrt(double x) {
+#if RT_FAST_SQRT
+  // 2^-767 <= x < inf  <=>  high word in [0x10000000, 0x7ff00000) (sign clear; one compare)
+  if (wave_all((uint32_t)__double2hiint(x) - 0x10000000u < 0x6ff00000u)) return sqrt_core(x);
+#endif
+  return __builtin_sqrt(x);
+}
+__device__ __forceinline__ double len(d3 v) { return gsqrt(v.x * v.x + v.y * v.y + v.z * v.z); }  // vec.go:95
 // Shared-denominator division, bit-identical to `/`. hipcc lowers an FP64
 // division on gfx950 to
 //   d' = div_scale(d); y = rcp(d'); 2x { e = fma(-d', y, 1); y = fma(y, e, y) }
 //   n' = div_scale(n); q = n' * y; r = fma(-d', q, n'); div_fmas(r, y, q); div_fixup
-// When 2^-400 <= |n|, |d| < 2^400 both div_scale steps are the identity
-// (VCC = 0, so div_fmas is a plain fma) and div_fixup returns its input, so
-// the reciprocal refinement depends on d alone and can be shared by several
-// numerators: 5 instructions once + 3 per quotient instead of 11 each.
-// Lanes outside that range take the real division in a wave-uniform branch.
-__device__ __forceinline__ bool div_safe(double x) {
-  const uint32_t h = (uint32_t)__double2hiint(x) & 0x7fffffffu;
-  return h - 0x26F00000u < 0x32000000u;  // biased exponent in [623, 1423)
-}
+// div_scale rescales by a power of two only to keep y, q and the residual r
+// out of the subnormal range, div_fmas undoes it, and div_fixup handles zero /
+// inf / NaN operands. For d in [2^-100, 2^100) and n = +-0 or |n| >= 2^-800,
+// y, q = n*y and r (zero, or a multiple of ulp(d)*ulp(q) >= 2^-904) are all
+// normal or zero, so the unscaled sequence rounds exactly as the scaled one
+// (round-to-nearest commutes with power-of-two scaling in the normal range),
+// and the reciprocal depends on d alone: the three quotients of a
+// normalisation share it. A zero numerator gives r = +0 and a +0 quotient
+// where div_fixup returns the numerator's sign: copysign restores it. A wave
+// takes this path when every active lane qualifies (each condition is one
+// compare, balloted on its own), else the hardware divisions.
 __device__ __forceinline__ double rcp_refined(double d) {
   double y = __builtin_amdgcn_rcp(d);
   double e = __builtin_fma(-d, y, 1.0);
@@ -45,31 +81,28 @@ __device__ __forceinline__ double rcp_refined(double d) {
   e = __builtin_fma(-d, y, 1.0);
   return __builtin_fma(y, e, y);
 }
-// A zero residual means q is the exact quotient: return it as is, which also
-// keeps the sign of a zero numerator (div_fmas would give +0 for n = -0, and
-// div_fixup restores the sign), so zero numerators need no fallback.
 __device__ __forceinline__ double div_rcp(double n, double d, double y) {
   const double q = n * y;
-  const double e = __builtin_fma(-d, q, n);
-  return e == 0.0 ? q : __builtin_fma(e, y, q);
+  return __builtin_copysign(__builtin_fma(__builtin_fma(-d, q, n), y, q), n);
 }
-__device__ __forceinline__ bool num_safe(double n) { return n == 0.0 || div_safe(n); }
-#ifndef RT_SHARED_DIV
-#define RT_SHARED_DIV 0  // measured slower on C3 (4.74 vs 4.56 ms): code size and selects outweigh the saved FP64 ops
+__device__ __forceinline__ uint64_t num_ok(double n) {
+  return __builtin_amdgcn_ballot_w64(__builtin_fabs(n) >= 0x1p-800) | __builtin_amdgcn_ballot_w64(n == 0.0);
+}
+#ifndef RT_FAST_NORM
+#define RT_FAST_NORM 0  // measured: fewer VALU but more scalar branch work, no faster
 #endif
 __device__ __forceinline__ d3 norm(d3 v) {                                                        // vec.go:78
-  double m = __builtin_sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
-#if RT_SHARED_DIV
-  const double y = rcp_refined(m);
-  d3 r = mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
-  const bool ok = div_safe(m) && num_safe(v.x) && num_safe(v.y) && num_safe(v.z);
-  if (__any(!ok)) {
-    if (!ok) r = mk(v.x / m, v.y / m, v.z / m);
+  double m = gsqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+#if RT_FAST_NORM
+  // d in [2^-100, 2^100): high word in [0x39B00000, 0x46300000) (one compare)
+  const uint64_t ok = __builtin_amdgcn_ballot_w64((uint32_t)__double2hiint(m) - 0x39B00000u < 0x0C800000u) &
+                      num_ok(v.x) & num_ok(v.y) & num_ok(v.z);
+  if (ok == __builtin_amdgcn_read_exec()) {
+    const double y = rcp_refined(m);
+    return mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
   }
-  return r;
-#else
-  return mk(v.x / m, v.y / m, v.z / m);
 #endif
+  return mk(v.x / m, v.y / m, v.z / m);
 }
 __device__ __forceinline__ d3 neg(d3 v) { return mk(-v.x, -v.y, -v.z); }                          // vec.go:87
 __device__ __forceinline__ d3 lerp(d3 a, d3 b, double t) {                                        // vec.go:56

@@ -26,7 +26,9 @@
 #define RT_SHADE_DEN 4
 #endif
 #ifndef RT_DIV_SKIP
-#define RT_DIV_SKIP 1  // skip divisions whose sign already proves t <= 0 (exact, see t_nonpos)
+#define RT_DIV_SKIP 0  // skip divisions whose sign proves t <= 0 (exact, see t_nonpos): measured
+                       // slower -- a skip pays only when the whole wave skips, the tests and
+                       // branches are paid always
 #endif
 #ifndef RT_FRAME_PREFETCH
 #define RT_FRAME_PREFETCH 1  // load the parent frame during the TRACE pass
@@ -36,6 +38,9 @@
 #endif
 #ifndef RT_STMAX_F32
 #define RT_STMAX_F32 0  // shadow-ray cull bound dist/|d| from an FP32 reciprocal (exact: bound only)
+#endif
+#ifndef RT_BRANCHFREE
+#define RT_BRANCHFREE 0  // straight-line Intersect routines: measured -35M scalar, +45M vector instructions on C3, no faster
 #endif
 #ifndef RT_CUBE_FAST
 #define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
@@ -177,7 +182,7 @@ __device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
   double c = dot(l.o, l.o) - 1.0;
   double disc = hb * hb - a * c;
   if (disc < 0.0) return false;
-  double sq = __builtin_sqrt(disc);
+  double sq = gsqrt(disc);
   double num = -hb - sq;
   if (t_nonpos(num, a)) return false;  // t0 <= 0: no near hit
   double t0 = num / a;
@@ -286,7 +291,7 @@ __device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, 
   if (__builtin_fabs(a) > 1e-12) {  // cylinder: a >= 0, the reference's a > 1e-12
     double disc = hb * hb - a * c0;
     if (disc >= 0.0) {
-      double sq = __builtin_sqrt(disc);
+      double sq = gsqrt(disc);
       // consider() ignores t <= 0 (raytracer.go:287), so a root whose sign is
       // known to be non-positive needs no division.
       double n0 = -hb - sq, n1 = -hb + sq;
@@ -345,14 +350,102 @@ __device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, 
 }
 
 
+#if RT_BRANCHFREE
+// Branch-free forms of the tests above: the same operations in the same
+// order, every candidate computed and the reference's accept/reject
+// decisions applied as masks and selects (a rejected candidate's division or
+// sqrt has no side effect). On a SIMD machine a per-lane early return only
+// saves work when the whole wave takes it, while its exec-mask bookkeeping
+// is paid every time; the kernel's cost is its instruction count.
+__device__ __forceinline__ bool sphere_hit_bf(const Ray& l, double& t) {  // raytracer.go:58-104
+  const double a = dot(l.d, l.d);
+  const double hb = dot(l.o, l.d);
+  const double c = dot(l.o, l.o) - 1.0;
+  const double disc = hb * hb - a * c;
+  const double t0 = (-hb - __builtin_sqrt(disc)) / a;
+  t = t0;
+  return !(disc < 0.0) & (t0 > 0.0);
+}
+__device__ __forceinline__ bool plane_hit_bf(const Ray& l, d3 n, double pd, double& t) {  // raytracer.go:164-180
+  const double denom = dot(n, l.d);
+  const double tt = (-pd - dot(n, l.o)) / denom;
+  t = tt;
+  return !(__builtin_fabs(denom) < 1e-6) & !(tt <= 0.0);
+}
+__device__ __forceinline__ bool cube_hit_bf(const Ray& l, double& t, int& face) {  // raytracer.go:214-240
+  bool found = false;
+  double best = 0.0;
+  int bf = 0;
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    const int ax = (f < 2) ? 2 : ((f < 4) ? 0 : 1);
+    const bool pos = (f == 1 || f == 3 || f == 4);
+    const double negD = pos ? 1.0 : 0.0;
+    const double dA = ax == 0 ? l.d.x : (ax == 1 ? l.d.y : l.d.z);
+    const double oA = ax == 0 ? l.o.x : (ax == 1 ? l.o.y : l.o.z);
+    const double denom = pos ? dA : -dA;
+    const double tt = (negD - (pos ? oA : -oA)) / denom;
+    const d3 p = add(l.o, scale(l.d, tt));
+    const bool ok = !(__builtin_fabs(denom) < 1e-6) & !(tt <= 0.0) & !(p.x < 0) & !(p.x > 1) & !(p.y < 0) &
+                    !(p.y > 1) & !(p.z < 0) & !(p.z > 1);
+    const bool upd = ok & (!found | (tt < best));
+    best = upd ? tt : best;
+    bf = upd ? f : bf;
+    found = found | ok;
+  }
+  t = best;
+  face = bf;
+  return found;
+}
+__device__ __forceinline__ bool cylinder_hit_bf(const Ray& l, double& t, int& face) {  // raytracer.go:279-337
+  double bestT = __builtin_inf();
+  int bestFace = -1;
+  const double a = l.d.x * l.d.x + l.d.z * l.d.z;
+  const double hb = l.o.x * l.d.x + l.o.z * l.d.z;
+  const double c0 = (l.o.x * l.o.x + l.o.z * l.o.z) - 1.0;
+  const double disc = hb * hb - a * c0;
+  const bool side = (__builtin_fabs(a) > 1e-12) & (disc >= 0.0);
+  const double sq = __builtin_sqrt(disc);
+  const double t0 = (-hb - sq) / a, t1 = (-hb + sq) / a;
+  const double y0 = l.o.y + l.d.y * t0, y1 = l.o.y + l.d.y * t1;
+  const bool h0 = side & (y0 >= 0.0) & (y0 <= 1.0) & (t0 > 0.0) & (t0 < bestT);
+  bestT = h0 ? t0 : bestT;
+  bestFace = h0 ? 0 : bestFace;
+  const bool h1 = side & (y1 >= 0.0) & (y1 <= 1.0) & (t1 > 0.0) & (t1 < bestT);
+  bestT = h1 ? t1 : bestT;
+  bestFace = h1 ? 0 : bestFace;
+  const bool caps = __builtin_fabs(l.d.y) > 1e-12;
+  const double tTop = (1.0 - l.o.y) / l.d.y;
+  const double pxT = l.o.x + l.d.x * tTop, pzT = l.o.z + l.d.z * tTop;
+  const bool hT = caps & (pxT * pxT + pzT * pzT <= 1.0) & (tTop > 0.0) & (tTop < bestT);
+  bestT = hT ? tTop : bestT;
+  bestFace = hT ? 1 : bestFace;
+  const double tBot = -l.o.y / l.d.y;
+  const double pxB = l.o.x + l.d.x * tBot, pzB = l.o.z + l.d.z * tBot;
+  const bool hB = caps & (pxB * pxB + pzB * pzB <= 1.0) & (tBot > 0.0) & (tBot < bestT);
+  bestT = hB ? tBot : bestT;
+  bestFace = hB ? 2 : bestFace;
+  t = bestT;
+  face = bestFace;
+  return bestFace >= 0;
+}
+#endif
+
 // One SceneObject.Intersect on a world-space ray; k is wave-uniform.
 __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r, double& t, int& face) {
   Ray l = to_obj(g, r);
   face = 0;
   // (kinds the specialised scene lacks fold away; the generic build keeps all)
+#if RT_BRANCHFREE
+  if (spec_kind(RT_SPHERE) && k == RT_SPHERE) return sphere_hit_bf(l, t);
+  if (spec_kind(RT_PLANE) && k == RT_PLANE) return plane_hit_bf(l, mk(g[12], g[13], g[14]), g[15], t);
+  if (spec_kind(RT_CUBE) && k == RT_CUBE) return cube_hit_bf(l, t, face);
+  if (spec_kind(RT_CYLINDER) && k == RT_CYLINDER) return cylinder_hit_bf(l, t, face);
+#else
   if (spec_kind(RT_SPHERE) && k == RT_SPHERE) return sphere_hit(l, t);
   if (spec_kind(RT_PLANE) && k == RT_PLANE) return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
   if (spec_kind(RT_CUBE) && k == RT_CUBE) return cube_hit(l, t, face);
+#endif
   if (!spec_kind(RT_CYLINDER) && !spec_kind(RT_CONE)) return false;  // unreachable for the scene's kinds
   return quadric_hit(l, t, face, spec_kind(RT_CONE) && (!spec_kind(RT_CYLINDER) || k == RT_CONE));
 }
@@ -1597,7 +1690,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           double cosI = -dot(nn, ray.d);
           double sinT2 = ratio * ratio * (1.0 - cosI * cosI);
           if (!(sinT2 > 1.0)) {
-            double cosT = __builtin_sqrt(1.0 - sinT2);
+            double cosT = gsqrt(1.0 - sinT2);
             d3 td = add(scale(ray.d, ratio), scale(nn, ratio * cosI - cosT));
             if (!iszero(td)) {
               hasT = true;
