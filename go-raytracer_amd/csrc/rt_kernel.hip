@@ -37,6 +37,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -571,6 +572,77 @@ struct SpecKey {
   }
 };
 
+// CSG membership program for the device (csg_eval): the composite's postfix
+// program (include/rt_abi.h RT_CSG) with every maximal union-only or
+// intersect-only group of leaf operands collapsed into one test of the
+// leaves' inside mask -- RT_CSG_ANY (some bit set) / RT_CSG_ALL (all set),
+// each followed by four 32-bit words of leaf bits -- and other operands kept
+// as they are. Union and intersection are associative and commutative, so the
+// boolean result is the original program's; "cube minus a union of 64
+// spheres" becomes three steps instead of 129.
+void csg_mask_program(const int* code, int len, std::vector<int>& out) {
+  struct Node {
+    int op, l, r;
+  };
+  std::vector<Node> nodes;
+  std::vector<int> st;
+  for (int k = 0; k < len; k++) {
+    const int op = code[k];
+    if (op >= 0) {
+      nodes.push_back({op, -1, -1});
+    } else {
+      const int r = st.back();
+      st.pop_back();
+      const int l = st.back();
+      st.pop_back();
+      nodes.push_back({op, l, r});
+    }
+    st.push_back((int)nodes.size() - 1);
+  }
+  std::function<void(int)> emit = [&](int n) {
+    const Node& nd = nodes[n];
+    if (nd.op >= 0) {
+      out.push_back(nd.op);
+      return;
+    }
+    if (nd.op == RT_CSG_DIFFERENCE) {
+      emit(nd.l);
+      emit(nd.r);
+      out.push_back(RT_CSG_DIFFERENCE);
+      return;
+    }
+    std::vector<int> leaves, others;
+    std::function<void(int)> flat = [&](int x) {
+      if (nodes[x].op == nd.op) {
+        flat(nodes[x].l);
+        flat(nodes[x].r);
+      } else if (nodes[x].op >= 0) {
+        leaves.push_back(nodes[x].op);
+      } else {
+        others.push_back(x);
+      }
+    };
+    flat(n);
+    bool first = true;
+    if (leaves.size() == 1) {
+      out.push_back(leaves[0]);
+      first = false;
+    } else if (leaves.size() > 1) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int j : leaves) w[j >> 5] |= 1u << (j & 31);
+      out.push_back(nd.op == RT_CSG_UNION ? RT_CSG_ANY : RT_CSG_ALL);
+      for (int q = 0; q < 4; q++) out.push_back((int)w[q]);
+      first = false;
+    }
+    for (int x : others) {
+      emit(x);
+      if (!first) out.push_back(nd.op);
+      first = false;
+    }
+  };
+  emit(st.back());
+}
+
 // Scene blob staged in LDS (small scenes) or read from global memory with
 // wave-uniform scalar loads. RT_SCENE_GLOBAL=1 forces the global flavour
 // (tuning experiments only).
@@ -967,6 +1039,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       }
     }
   }
+  std::vector<int> mcode;  // device membership programs (csg_mask_program)
   // CSG composites: bounding sphere from the leaves (union: enclosing sphere,
   // intersect: the smaller operand, difference: the left operand; a plane leaf
   // is unbounded), leaf range and program in geo slots 14..15.
@@ -1028,8 +1101,9 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     int* ci = reinterpret_cast<int*>(&g[14]);
     ci[0] = o.csg_first;
     ci[1] = o.csg_count;
-    ci[2] = o.csg_code;
-    ci[3] = o.csg_code_len;
+    ci[2] = (int)mcode.size();
+    csg_mask_program(in->csg_code + o.csg_code, o.csg_code_len, mcode);
+    ci[3] = (int)mcode.size() - ci[2];
     s.has_csg = true;
   }
   std::vector<double> mats((size_t)s.nmats * MAT, 0.0);
@@ -1155,7 +1229,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   }
   s.off_prefb = align16(s.off_objmat + (int)(objmat.size() * sizeof(int)));
   s.off_csg = align16(s.off_prefb + (int)(prefb.size() * sizeof(uint32_t)));
-  s.off_code = align16(s.off_csg + ncsg * (int)sizeof(int));
+  s.off_code = align16(s.off_csg + (int)(mcode.size() * sizeof(int)));
   s.off_consts = align16(s.off_code + ncode * (int)sizeof(uint32_t));
   s.off_entry = align16(s.off_consts + nconst * (int)sizeof(uint64_t));
   s.blob_bytes = align16(s.off_entry + nprog * (int)sizeof(int));
@@ -1168,7 +1242,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     std::memcpy(blob.data() + s.off_kind, kind.data(), kind.size() * sizeof(int));
     std::memcpy(blob.data() + s.off_objmat, objmat.data(), objmat.size() * sizeof(int));
     std::memcpy(blob.data() + s.off_prefb, prefb.data(), prefb.size() * sizeof(uint32_t));
-    if (ncsg) std::memcpy(blob.data() + s.off_csg, in->csg_code, (size_t)ncsg * sizeof(int));
+    if (!mcode.empty()) std::memcpy(blob.data() + s.off_csg, mcode.data(), mcode.size() * sizeof(int));
     if (nprog) {
       std::memcpy(blob.data() + s.off_code, in->program_code, (size_t)ncode * sizeof(uint32_t));
       std::memcpy(blob.data() + s.off_consts, in->program_consts, (size_t)nconst * sizeof(uint64_t));

@@ -611,10 +611,13 @@ __device__ __forceinline__ void leaf_interval(int kind, const double* g, const R
   f = fa | (fb << 4) | (ok ? 256 : 0);
 }
 
-// Postfix membership of the composite just before (after = false) or just
-// after t (bit stacks, depth <= RT_CSG_MAX_LEAVES).
-__device__ __forceinline__ bool csg_member(const int* code, int n, const double* A, const double* B, uint64_t live0,
-                                           uint64_t live1, double t, bool after) {
+// Membership of the composite given its leaves' inside mask m (bit j: leaf j
+// contains the point), by the host-compiled program (rt_kernel.hip
+// csg_mask_program): the postfix program with union-only / intersect-only
+// groups of leaves collapsed into one mask test (bit stacks, depth <=
+// RT_CSG_MAX_LEAVES).
+enum { RT_CSG_ANY = -4, RT_CSG_ALL = -5 };
+__device__ __forceinline__ bool csg_eval(const int* code, int n, uint64_t m0, uint64_t m1) {
   uint64_t st0 = 0, st1 = 0;
   int sp = 0;
   auto get = [&](int i) -> bool { return ((i < 64 ? st0 >> i : st1 >> (i - 64)) & 1) != 0; };
@@ -626,17 +629,21 @@ __device__ __forceinline__ bool csg_member(const int* code, int n, const double*
   };
   for (int k = 0; k < n; k++) {
     const int op = code[k];
+    bool v;
     if (op >= 0) {
-      const bool live = ((op < 64 ? live0 >> op : live1 >> (op - 64)) & 1) != 0;  // no load for culled leaves
-      const bool in = live && (after ? (A[op] <= t && t < B[op]) : (A[op] < t && t <= B[op]));
-      set(sp, in);
-      sp++;
+      v = ((op < 64 ? m0 >> op : m1 >> (op - 64)) & 1) != 0;
+    } else if (op <= RT_CSG_ANY) {
+      const uint64_t k0 = (uint32_t)code[k + 1] | ((uint64_t)(uint32_t)code[k + 2] << 32);
+      const uint64_t k1 = (uint32_t)code[k + 3] | ((uint64_t)(uint32_t)code[k + 4] << 32);
+      k += 4;
+      v = op == RT_CSG_ANY ? ((m0 & k0) | (m1 & k1)) != 0 : ((m0 & k0) == k0 && (m1 & k1) == k1);
     } else {
       sp -= 2;
       const bool x = get(sp), y = get(sp + 1);
-      set(sp, op == RT_CSG_UNION ? (x || y) : (op == RT_CSG_INTERSECT ? (x && y) : (x && !y)));
-      sp++;
+      v = op == RT_CSG_UNION ? (x || y) : (op == RT_CSG_INTERSECT ? (x && y) : (x && !y));
     }
+    set(sp, v);
+    sp++;
   }
   return (st0 & 1) != 0;
 }
@@ -698,8 +705,26 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
     }
     if (je < 0) return false;
     if (cut_strict ? te * cut_m > cut_lim : te * cut_m >= cut_lim) return false;
-    const bool before = csg_member(prog, plen, A, B, live0, live1, te, false),
-               after = csg_member(prog, plen, A, B, live0, live1, te, true);
+    // leaves containing the points just before / just after te
+    uint64_t b0 = 0, b1 = 0, a0 = 0, a1 = 0;
+    for (int w = 0; w < 2; w++) {
+      uint64_t m = w ? live1 : live0, bm = 0, am = 0;
+      while (m) {
+        const int q = __builtin_ctzll(m);
+        m &= m - 1;
+        const int j = w * 64 + q;
+        if (A[j] < te && te <= B[j]) bm |= 1ull << q;
+        if (A[j] <= te && te < B[j]) am |= 1ull << q;
+      }
+      if (w) {
+        b1 = bm;
+        a1 = am;
+      } else {
+        b0 = bm;
+        a0 = am;
+      }
+    }
+    const bool before = csg_eval(prog, plen, b0, b1), after = csg_eval(prog, plen, a0, a1);
     if (before != after) {
       const int flip = ((jend == 0) != after) ? 1 : 0;
       t = te;
