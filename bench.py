@@ -28,6 +28,7 @@ from __graft_entry__ import load_package  # noqa: E402
 PEAK_FP64_TFLOPS = 78.6
 PEAK_FP64_NOFMA_TFLOPS = 39.3  # parity build: no contraction -> one mul or add per lane-op
 PEAK_HBM_GBS = 8000.0
+METRIC = "Mrays/s (primary+shadow+reflect) at 4K depth=6; 1/2/4/8-GPU scaling"  # BASELINE.json "metric"
 
 
 def parse():
@@ -159,7 +160,7 @@ def main():
         achieved_tf = flops_per_launch / (kavg * 1e-3) / 1e12 if kavg > 0 else 0.0
         out_bytes = dr.buf.numel()
         line = {
-            "metric": "Mrays/s (primary+shadow+reflect) at 4K depth=6",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
