@@ -46,6 +46,9 @@ def parse():
                         "strong: one frame's rows sharded over the ranks + gather")
     p.add_argument("--shard", choices=["interleaved", "bands"], default="interleaved",
                    help="row partition for --scaling strong")
+    p.add_argument("--accel", choices=["bvh", "none"], default="bvh",
+                   help="none: the reference's brute-force search (no BVH, no culling; identical pixels "
+                        "and counters) -- BASELINE config 5's regime, the FP64 roofline of the Intersect loop")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -114,6 +117,8 @@ def main():
     rargs = cfg(**kw)
     packed = pkg.scene.convert(rargs)
     ctx = pkg.RenderContext(local, specialize=args.specialize == "on")
+    if args.accel == "none":
+        ctx.set_accel(0)
     ctx.set_scene(packed)
     spec_active, spec_ms = ctx.specialized()
     mode = "frame" if args.scaling == "weak" else args.shard
@@ -179,6 +184,7 @@ def main():
                        "parallelism": ("frame-per-gpu%d" % world) if args.scaling == "weak"
                                       else "rows%d-%s" % (world, args.shard),
                        "kernel": "specialised" if spec_active else "generic",
+                       "accel": "bvh+cull" if args.accel == "bvh" else "none (brute force)",
                        "spec_compile_ms": round(spec_ms, 1)},
             "roofline": {"bound": "valu-fp64", "achieved": round(achieved_tf, 3), "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),

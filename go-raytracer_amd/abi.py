@@ -20,6 +20,7 @@ KIND_NAMES = ("sphere", "plane", "cube", "cylinder", "cone", "csg")
 RT_CSG_UNION, RT_CSG_INTERSECT, RT_CSG_DIFFERENCE = -1, -2, -3
 RT_CSG_MAX_LEAVES = 128
 RT_SPEC_SURFACES, RT_SPEC_DIRECTIONAL, RT_SPEC_SPOT = 1, 2, 4  # rt_spec_precompile feature bits
+RT_ACCEL_BVH, RT_ACCEL_CULL = 1, 2  # rt_set_accel flags
 
 
 def RT_SPEC_LIGHTS(n):

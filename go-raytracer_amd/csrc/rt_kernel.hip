@@ -447,6 +447,7 @@ struct rt_context {
   uint64_t primary_pending = 0;  // host-side count of launched primary rays
   // scene specialisation (rt_set_specialize)
   bool specialize = false;
+  int accel = RT_ACCEL_BVH | RT_ACCEL_CULL;  // rt_set_accel
   hipFunction_t spec_fn = nullptr;  // specialised kernel of the current scene, if any
   double spec_ms = 0;               // hipRTC compile time of spec_fn (0 = cache hit)
 };
@@ -566,9 +567,11 @@ struct SpecKey {
   std::string kinds;
   int kmask = 0, feat = 0, nlights = 0;  // nlights > 0: light loop unrolled for that count
   int pow_bits = 7;                      // unrolled specular powering steps
+  int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
   std::string str() const {
     return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
-           std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits);
+           std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits) +
+           ":" + std::to_string(nocull);
   }
 };
 
@@ -685,6 +688,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   }
   if (sk.nlights > 0) defs.push_back("-DRT_SPEC_NLIGHTS=" + std::to_string(sk.nlights));
   defs.push_back("-DRT_SPEC_POWBITS=" + std::to_string(sk.pow_bits));
+  if (sk.nocull) defs.push_back("-DRT_CULL=0");
   std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
   for (const auto& d : defs) opts.push_back(d.c_str());
   // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only)
@@ -769,6 +773,7 @@ int spec_prepare(rt_context* c) {
   if (!c->specialize || !c->has_scene) return RT_OK;
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
+  sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
   std::lock_guard<std::mutex> lock(g_spec_mu);
   return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
 }
@@ -778,6 +783,13 @@ int spec_prepare(rt_context* c) {
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_set_accel(rt_context* c, int flags) {
+  if (!c) return fail(RT_E_INVALID, "rt_set_accel: NULL context");
+  if (flags & ~(RT_ACCEL_BVH | RT_ACCEL_CULL)) return fail(RT_E_INVALID, "rt_set_accel: unknown flags");
+  c->accel = flags;
+  return spec_prepare(c);
+}
 
 int rt_set_specialize(rt_context* c, int enable) {
   if (!c) return fail(RT_E_INVALID, "rt_set_specialize: NULL context");
@@ -1260,7 +1272,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     std::vector<int> bounded, planes;
     for (int i = 0; i < s.nobj; i++) (kind[i] == RT_PLANE || kind[i] == RT_CSG ? planes : bounded).push_back(i);
     BvhBuild b;
-    if ((int)bounded.size() >= RT_BVH_MIN) {
+    if ((c->accel & RT_ACCEL_BVH) && (int)bounded.size() >= RT_BVH_MIN) {
       b.c = &bcen;
       b.r = &brad;
       b.geo = &geo;

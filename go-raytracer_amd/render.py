@@ -61,6 +61,8 @@ def load_library(path=None):
     l.rt_ssim_rgba8.restype = i
     l.rt_set_specialize.argtypes = [vp, i]
     l.rt_set_specialize.restype = i
+    l.rt_set_accel.argtypes = [vp, i]
+    l.rt_set_accel.restype = i
     l.rt_specialized.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
     l.rt_specialized.restype = i
     l.rt_spec_precompile.argtypes = [i, C.POINTER(i), i, C.POINTER(C.c_double)]
@@ -124,6 +126,13 @@ class RenderContext:
         their object kinds (hipRTC, ~1-2 s once per scene shape and process;
         bit-identical output). Raises RenderError if hipRTC fails."""
         _check(self.lib.rt_set_specialize(self.handle, int(bool(enable))), "rt_set_specialize")
+
+    def set_accel(self, flags):
+        """abi.RT_ACCEL_BVH | abi.RT_ACCEL_CULL (default both). 0 = the
+        reference's brute-force search (every ray tests every object in FP64;
+        identical pixels and counters). The BVH choice applies at the next
+        set_scene; culling applies to specialised kernels."""
+        _check(self.lib.rt_set_accel(self.handle, int(flags)), "rt_set_accel")
 
     def specialized(self):
         """(active, compile_ms): whether the current scene runs a specialised

@@ -259,6 +259,17 @@ int rt_last_kernel_ms(rt_context *ctx, double *ms_out);
  * Takes effect immediately for the current scene and in every rt_set_scene. */
 int rt_set_specialize(rt_context *ctx, int enable);
 
+/* Acceleration of the exact search (MI355X-specific; pixels and counters are
+ * identical either way): RT_ACCEL_BVH builds a BVH over the bounded objects of
+ * scenes with >= 12 of them (takes effect at the next rt_set_scene);
+ * RT_ACCEL_CULL lets the kernel skip Intersect calls an FP32 bound proves to
+ * miss (specialised kernels only; the generic kernel always culls). Default:
+ * both. 0 runs the reference's brute-force search -- every ray tests every
+ * object in FP64 -- e.g. to measure the FP64 roofline of the Intersect loop. */
+#define RT_ACCEL_BVH 1
+#define RT_ACCEL_CULL 2
+int rt_set_accel(rt_context *ctx, int flags);
+
 /* Whether the current scene runs a specialised kernel, and the compile time
  * (ms) that preparing it cost (0 on a cache hit). Either pointer may be NULL. */
 int rt_specialized(rt_context *ctx, int *active, double *compile_ms);

@@ -540,3 +540,29 @@ def test_specialised_full_4k_c3_equals_generic(ctx, spec_ctx):
     assert np.array_equal(a, c)
     spec_ctx.set_specialize(True)
     assert spec_ctx.specialized() == (True, 0.0)  # cached: no second compile
+
+
+# --- rt_set_accel: the reference's brute-force search (no BVH, no culling)
+# must give the same pixels and counters as the accelerated search.
+
+@pytest.mark.parametrize("case", ["c5", "mixed", "c3"])
+def test_brute_force_search_matches_oracle(case, spec_ctx):
+    if case == "c5":
+        args = rt.configs.c5(width=48, height=32, nx=6, ny=4, nz=2)  # 48 spheres + plane: BVH when accelerated
+    elif case == "mixed":
+        args = _mixed_scene(4, 40, 64, 48)
+    else:
+        args = rt.configs.c3(width=96, height=64)
+    packed = rt.scene.convert(args)
+    ref, ost = oracle_bind.render_rows(packed)
+    try:
+        spec_ctx.set_accel(0)
+        img, st = render(spec_ctx, packed)
+        assert spec_ctx.specialized()[0]
+        assert_same(img, ref, "brute force " + case)
+        assert st.as_dict() == ost.as_dict()
+    finally:
+        spec_ctx.set_accel(rt.abi.RT_ACCEL_BVH | rt.abi.RT_ACCEL_CULL)
+    img2, st2 = render(spec_ctx, packed)
+    assert np.array_equal(img, img2)
+    assert st.as_dict() == st2.as_dict()
