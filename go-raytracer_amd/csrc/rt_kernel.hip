@@ -1350,7 +1350,10 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
   const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * 12 : 0);
   const int jump_off = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
-  const int frames_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);
+  // per-wave object-record stream buffers (global linear scenes, RT_STREAM)
+  const int stream_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);
+  const bool use_stream = !lds && !s.use_bvh && !s.has_csg;
+  const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
   const void* kfn;
   if (s.has_csg)
@@ -1400,6 +1403,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.lds_frames_off = frames_off;
   P.lds_levels = lds_levels;
   P.lds_full = lds_full;
+  P.stream_off = stream_off;
   P.lds_ext_off = ext_off;
   P.jump_off = jump_off;
   P.off_geo = s.off_geo;

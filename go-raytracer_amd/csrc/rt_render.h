@@ -39,6 +39,9 @@
 #ifndef RT_STMAX_F32
 #define RT_STMAX_F32 0  // shadow-ray cull bound dist/|d| from an FP32 reciprocal (exact: bound only)
 #endif
+#ifndef RT_STREAM
+#define RT_STREAM 1  // global linear scenes: object records stream through per-wave LDS buffers
+#endif
 #ifndef RT_BRANCHFREE
 #define RT_BRANCHFREE 0  // straight-line Intersect routines: measured -35M scalar, +45M vector instructions on C3, no faster
 #endif
@@ -102,6 +105,7 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
 // material is both reflective and transparent) always live in HBM.
 enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
+enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
        ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32 };  // (stats buffer: 64 entries)
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
@@ -115,6 +119,7 @@ struct Params {
   int lds_levels;      // recursion levels whose frame core lives in LDS (host: LDS left at full occupancy)
   int lds_full;        // recursion levels whose other frame fields (3..11) live in LDS too
   int lds_ext_off;     // byte offset of those fields in dynamic LDS
+  int stream_off;      // byte offset of the per-wave object-record stream buffers (global linear scenes)
   int jump_off;        // byte offset of the LDS copy of the PCG jump table
   int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_csg, off_code, off_consts,
       off_entry, blob_bytes;
@@ -1013,6 +1018,50 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     vmrec = reinterpret_cast<double*>(smem + P.lds_vm_off) + (size_t)threadIdx.x * MAT;
   else
     vmrec = P.vm_global + ((size_t)wslot * 64 + lane) * MAT;
+  // Global linear scenes (scene too large for LDS, no BVH, no CSG): object
+  // records and kinds stream through a per-wave LDS buffer in chunks of SCH,
+  // the next chunk's 16-B loads in flight while the current chunk is tested
+  // (the in-order loop the reference runs, with the record latency hidden).
+  // body(i, kind, record) returns false to stop (a wave-uniform decision).
+  constexpr bool STREAM = !LDS && !BVH && !CSG && RT_STREAM;
+  double* sbuf = reinterpret_cast<double*>(smem + P.stream_off) + (size_t)(threadIdx.x >> 6) * (SCH * GEO);
+  int* skind = reinterpret_cast<int*>(smem + P.stream_off + WAVES_PER_WG * SCH * GEO * (int)sizeof(double)) +
+               (threadIdx.x >> 6) * SCH;
+  auto stream_objects = [&](auto&& body) {
+    constexpr int PER = SCH * GEO * (int)sizeof(double) / 16 / 64;  // 16-B pieces per lane per chunk
+    const uint4* src = reinterpret_cast<const uint4*>(S.geo);
+    uint4* dst = reinterpret_cast<uint4*>(sbuf);
+    const int lane_ = (int)(threadIdx.x & 63);
+    uint4 pre[PER];
+    int pk = 0;
+    auto fetch = [&](int c0) {
+      const int n16 = min(SCH, P.nobj - c0) * (GEO * (int)sizeof(double) / 16);
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const int idx = lane_ + q * 64;
+        pre[q] = idx < n16 ? src[(size_t)c0 * (GEO * sizeof(double) / 16) + idx] : make_uint4(0, 0, 0, 0);
+      }
+      pk = lane_ < min(SCH, P.nobj - c0) ? S.kind[c0 + lane_] : 0;
+    };
+    auto store = [&]() {
+#pragma unroll
+      for (int q = 0; q < PER; q++) dst[lane_ + q * 64] = pre[q];
+      if (lane_ < SCH) skind[lane_] = pk;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    };
+    if (P.nobj <= 0) return;
+    fetch(0);
+    store();
+    for (int c0 = 0; c0 < P.nobj; c0 += SCH) {
+      const int n = min(SCH, P.nobj - c0);
+      const bool more = c0 + SCH < P.nobj;
+      if (more) fetch(c0 + SCH);
+      for (int j = 0; j < n; j++)
+        if (!body(c0 + j, skind[j], sbuf + (size_t)j * GEO)) return;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane done reading the chunk
+      if (more) store();
+    }
+  };
   const d3 eye = mk(0.0, 0.0, -1.0);  // raytracer.go:605-609
 
   // lane state
@@ -1259,7 +1308,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           for (int i = 0; i < RT_SPEC_NOBJ; i++) trace_obj(i, spec_kinds[i], S.geo + (size_t)i * GEO, tr);
         }
 #else
-        for (int i = 0; i < P.nobj; i++) trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
+        if constexpr (STREAM) {
+          stream_objects([&](int i, int k, const double* g) {
+            trace_obj(i, k, g, tr);
+            return true;
+          });
+        } else {
+          for (int i = 0; i < P.nobj; i++) trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
+        }
 #endif
       } else {
         for (int p = 0; p < P.nplanes; p++) {  // unbounded objects: planes, unbounded CSG
@@ -1489,7 +1545,28 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           if (!__any(open)) break;
           const int k = spec_kinds[i];
 #else
-        for (int i = 0; i < P.nobj; i++) {
+        if constexpr (STREAM) {
+          stream_objects([&](int i, int k, const double* g) {
+            if (!__any(open)) return false;
+            bool test = open && i != hit_i;
+#if RT_CULL
+            test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
+                                          : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+            if (!__any(test)) return true;
+#endif
+            EXDIAG(k, 1, test);
+            if (test) {
+              double t;
+              int f;
+              if (object_hit(k, g, sr, t, f) && t * rlen < dist) {
+                open = false;
+                send = i + 1;
+              }
+            }
+            return true;
+          });
+        }
+        for (int i = STREAM ? P.nobj : 0; i < P.nobj; i++) {
           if (!__any(open)) break;
           const int k = S.kind[i];
 #endif
