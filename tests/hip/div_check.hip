@@ -2,7 +2,7 @@
 // equals three IEEE `/` bit for bit, on random vectors spanning the safe
 // exponent range, its edges and beyond (fallback path), plus zeros, signed
 // zeros, denormals, infinities and NaN components.
-// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -DRT_SHARED_DIV=1 -I../../go-raytracer_amd/csrc div_check.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -DRT_FAST_NORM=1 -I../../go-raytracer_amd/csrc div_check.hip
 #include "rt_device.h"
 #include <cstdio>
 #include <cstdlib>
@@ -39,7 +39,9 @@ __device__ double gen(uint64_t& s, int mode) {
 __global__ void check(uint64_t seed, int iters, unsigned long long* bad, unsigned long long* fast) {
   uint64_t s = seed ^ ((uint64_t)(blockIdx.x * blockDim.x + threadIdx.x) << 20);
   for (int it = 0; it < iters; it++) {
-    const int mode = (int)(mix(s ^ it) % 16);
+    // wave-uniform mode, so whole waves meet the fast-path preconditions
+    const uint64_t wave = (uint64_t)(blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int mode = (int)(mix(seed ^ (wave << 24) ^ (uint64_t)it) % 16);
     const int m = mode < 11 ? 0 : (mode < 13 ? 1 : (mode < 15 ? 2 : 3));
     d3 v = mk(gen(s, m), gen(s, m), gen(s, mode == 10 ? 3 : m));
     d3 a = norm(v);
@@ -59,7 +61,12 @@ __global__ void check(uint64_t seed, int iters, unsigned long long* bad, unsigne
                  b.z);
       }
     }
-    if (div_safe(mm) && div_safe(v.x) && div_safe(v.y) && div_safe(v.z)) atomicAdd(fast, 1ULL);
+    // lanes meeting the shared-reciprocal preconditions (norm takes that path
+    // when the whole wave does)
+    const bool num = (__builtin_fabs(v.x) >= 0x1p-800 || v.x == 0.0) &&
+                     (__builtin_fabs(v.y) >= 0x1p-800 || v.y == 0.0) &&
+                     (__builtin_fabs(v.z) >= 0x1p-800 || v.z == 0.0);
+    if (num && mm >= 0x1p-100 && mm < 0x1p100) atomicAdd(fast, 1ULL);
   }
 }
 
