@@ -33,7 +33,9 @@ __device__ __forceinline__ d3 scale(d3 a, double s) { return mk(a.x * s, a.y * s
 // test is false, so the core below gives the same bits in 10 instead of 18
 // VALU instructions; a wave takes it when all its lanes qualify.
 #ifndef RT_FAST_SQRT
-#define RT_FAST_SQRT 0  // measured: fewer VALU but more scalar branch work, no faster
+// 2: per-lane fix-up form (default; -2.6 % VALU, C3 -0.2..-1.2 %). 1:
+// wave-uniform form (more scalar branch work, no faster). 0: full sequence.
+#define RT_FAST_SQRT 2
 #endif
 __device__ __forceinline__ double sqrt_core(double x) {
   const double y = __builtin_amdgcn_rsq(x);
@@ -52,7 +54,12 @@ __device__ __forceinline__ bool wave_all(bool c) {
   return __builtin_amdgcn_ballot_w64(c) == __builtin_amdgcn_read_exec();
 }
 __device__ __forceinline__ double gsqrt(double x) {
-#if RT_FAST_SQRT
+#if RT_FAST_SQRT == 2
+  // every lane takes the core; lanes outside the range redo the full sequence
+  double g = sqrt_core(x);
+  if (__builtin_expect((uint32_t)__double2hiint(x) - 0x10000000u >= 0x6ff00000u, 0)) g = __builtin_sqrt(x);
+  return g;
+#elif RT_FAST_SQRT
   // 2^-767 <= x < inf  <=>  high word in [0x10000000, 0x7ff00000) (sign clear; one compare)
   if (wave_all((uint32_t)__double2hiint(x) - 0x10000000u < 0x6ff00000u)) return sqrt_core(x);
 #endif
@@ -89,11 +96,35 @@ __device__ __forceinline__ uint64_t num_ok(double n) {
   return __builtin_amdgcn_ballot_w64(__builtin_fabs(n) >= 0x1p-800) | __builtin_amdgcn_ballot_w64(n == 0.0);
 }
 #ifndef RT_FAST_NORM
-#define RT_FAST_NORM 0  // measured: fewer VALU but more scalar branch work, no faster
+// 2: per-lane fix-up form (default; C3 -2.3 % wave cycles). 1: wave-uniform
+// form (more scalar branch work). 0: hardware divisions.
+#define RT_FAST_NORM 2
 #endif
 __device__ __forceinline__ d3 norm(d3 v) {                                                        // vec.go:78
+#if RT_FAST_NORM == 2
+  // Every lane takes the core square root and the shared-reciprocal
+  // quotients; lanes outside their ranges redo both with the full hardware
+  // sequences under one (rarely entered) branch. x = m^2 in [2^-200, 2^198)
+  // puts x in the core sqrt range and m in [2^-100, 2^100) (sqrt is
+  // correctly rounded and monotone; 2^198 keeps a round-up to 2^100 out).
+  // Numerators: +-0 or |n| >= 2^-800 <=> frexp exponent >= -799 (a zero's
+  // exponent is 0, a denormal's < -1021; inf/NaN components fail on x).
+  const double x = v.x * v.x + v.y * v.y + v.z * v.z;
+  double m = sqrt_core(x);
+  const double y = rcp_refined(m);
+  d3 r = mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
+  const int en = min(min(__builtin_amdgcn_frexp_exp(v.x), __builtin_amdgcn_frexp_exp(v.y)),
+                     __builtin_amdgcn_frexp_exp(v.z));
+  const bool ok = ((uint32_t)__double2hiint(x) - 0x33700000u < 0x18E00000u) & (en > -800);
+  if (__builtin_expect(!ok, 0)) {
+    m = __builtin_sqrt(x);
+    r = mk(v.x / m, v.y / m, v.z / m);
+  }
+  return r;
+#else
   double m = gsqrt(v.x * v.x + v.y * v.y + v.z * v.z);
-#if RT_FAST_NORM
+#endif
+#if RT_FAST_NORM == 1
   // d in [2^-100, 2^100): high word in [0x39B00000, 0x46300000) (one compare)
   const uint64_t ok = __builtin_amdgcn_ballot_w64((uint32_t)__double2hiint(m) - 0x39B00000u < 0x0C800000u) &
                       num_ok(v.x) & num_ok(v.y) & num_ok(v.z);
@@ -102,7 +133,9 @@ __device__ __forceinline__ d3 norm(d3 v) {                                      
     return mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
   }
 #endif
+#if RT_FAST_NORM != 2
   return mk(v.x / m, v.y / m, v.z / m);
+#endif
 }
 __device__ __forceinline__ d3 neg(d3 v) { return mk(-v.x, -v.y, -v.z); }                          // vec.go:87
 __device__ __forceinline__ d3 lerp(d3 a, d3 b, double t) {                                        // vec.go:56

@@ -1,8 +1,9 @@
-// Device check (test infrastructure): rt::norm's shared-reciprocal division
-// equals three IEEE `/` bit for bit, on random vectors spanning the safe
-// exponent range, its edges and beyond (fallback path), plus zeros, signed
-// zeros, denormals, infinities and NaN components.
-// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -DRT_FAST_NORM=1 -I../../go-raytracer_amd/csrc div_check.hip
+// Device check (test infrastructure): rt::norm's core square root and
+// shared-reciprocal division equal IEEE sqrt and three `/` bit for bit, on
+// random vectors spanning the safe exponent range, its edges and beyond
+// (fix-up path), plus zeros, signed zeros, denormals, infinities and NaN
+// components.
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I../../go-raytracer_amd/csrc div_check.hip
 #include "rt_device.h"
 #include <cstdio>
 #include <cstdlib>
@@ -25,8 +26,9 @@ __device__ double gen(uint64_t& s, int mode) {
       const uint64_t e = (r >> 52) % 2047;
       return __longlong_as_double((long long)(((r & 1) << 63) | (e << 52) | (mix(r) & 0xFFFFFFFFFFFFFULL)));
     }
-    case 2: {  // around the safe-range edges
-      const int64_t e = (r & 2) ? 623 + (int64_t)((r >> 8) % 5) - 2 : 1423 + (int64_t)((r >> 8) % 5) - 2;
+    case 2: {  // around the safe-range edges (numerators 2^-800, m 2^-100 / 2^99, far out)
+      const int64_t edge[4] = {223, 923, 1122, 1423};
+      const int64_t e = edge[(r >> 1) & 3] + (int64_t)((r >> 8) % 5) - 2;
       return __longlong_as_double((long long)(((r & 1) << 63) | ((uint64_t)e << 52) | (mix(r) & 0xFFFFFFFFFFFFFULL)));
     }
     default: {  // specials
@@ -61,8 +63,7 @@ __global__ void check(uint64_t seed, int iters, unsigned long long* bad, unsigne
                  b.z);
       }
     }
-    // lanes meeting the shared-reciprocal preconditions (norm takes that path
-    // when the whole wave does)
+    // lanes meeting the fast-path preconditions (the others take the fix-up)
     const bool num = (__builtin_fabs(v.x) >= 0x1p-800 || v.x == 0.0) &&
                      (__builtin_fabs(v.y) >= 0x1p-800 || v.y == 0.0) &&
                      (__builtin_fabs(v.z) >= 0x1p-800 || v.z == 0.0);
