@@ -31,7 +31,7 @@ __device__ __forceinline__ d3 scale(d3 a, double s) { return mk(a.x * s, a.y * s
 //   result = class(x', +-0 | +inf) ? x' : g
 // For 2^-767 <= x < inf the scaling steps are the identity and the class
 // test is false, so the core below gives the same bits in 10 instead of 18
-// VALU instructions; a wave takes it when all its lanes qualify.
+// VALU instructions.
 #ifndef RT_FAST_SQRT
 // 2: per-lane fix-up form (default; -2.6 % VALU, C3 -0.2..-1.2 %). 1:
 // wave-uniform form (more scalar branch work, no faster). 0: full sequence.
@@ -78,9 +78,7 @@ __device__ __forceinline__ double len(d3 v) { return gsqrt(v.x * v.x + v.y * v.y
 // (round-to-nearest commutes with power-of-two scaling in the normal range),
 // and the reciprocal depends on d alone: the three quotients of a
 // normalisation share it. A zero numerator gives r = +0 and a +0 quotient
-// where div_fixup returns the numerator's sign: copysign restores it. A wave
-// takes this path when every active lane qualifies (each condition is one
-// compare, balloted on its own), else the hardware divisions.
+// where div_fixup returns the numerator's sign: copysign restores it.
 __device__ __forceinline__ double rcp_refined(double d) {
   double y = __builtin_amdgcn_rcp(d);
   double e = __builtin_fma(-d, y, 1.0);
@@ -100,7 +98,8 @@ __device__ __forceinline__ uint64_t num_ok(double n) {
 // form (more scalar branch work). 0: hardware divisions.
 #define RT_FAST_NORM 2
 #endif
-__device__ __forceinline__ d3 norm(d3 v) {                                                        // vec.go:78
+// norm(v) that also hands back |v| (the same bits as len(v)).
+__device__ __forceinline__ d3 norm_len(d3 v, double& m) {                                        // vec.go:78,95
 #if RT_FAST_NORM == 2
   // Every lane takes the core square root and the shared-reciprocal
   // quotients; lanes outside their ranges redo both with the full hardware
@@ -110,7 +109,7 @@ __device__ __forceinline__ d3 norm(d3 v) {                                      
   // Numerators: +-0 or |n| >= 2^-800 <=> frexp exponent >= -799 (a zero's
   // exponent is 0, a denormal's < -1021; inf/NaN components fail on x).
   const double x = v.x * v.x + v.y * v.y + v.z * v.z;
-  double m = sqrt_core(x);
+  m = sqrt_core(x);
   const double y = rcp_refined(m);
   d3 r = mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
   const int en = min(min(__builtin_amdgcn_frexp_exp(v.x), __builtin_amdgcn_frexp_exp(v.y)),
@@ -122,7 +121,7 @@ __device__ __forceinline__ d3 norm(d3 v) {                                      
   }
   return r;
 #else
-  double m = gsqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+  m = gsqrt(v.x * v.x + v.y * v.y + v.z * v.z);
 #endif
 #if RT_FAST_NORM == 1
   // d in [2^-100, 2^100): high word in [0x39B00000, 0x46300000) (one compare)
@@ -136,6 +135,10 @@ __device__ __forceinline__ d3 norm(d3 v) {                                      
 #if RT_FAST_NORM != 2
   return mk(v.x / m, v.y / m, v.z / m);
 #endif
+}
+__device__ __forceinline__ d3 norm(d3 v) {  // vec.go:78
+  double m;
+  return norm_len(v, m);
 }
 __device__ __forceinline__ d3 neg(d3 v) { return mk(-v.x, -v.y, -v.z); }                          // vec.go:87
 __device__ __forceinline__ d3 lerp(d3 a, d3 b, double t) {                                        // vec.go:56

@@ -1513,8 +1513,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         dist = __builtin_inf();
       } else {
         d3 lth = sub(mk(lt[0], lt[1], lt[2]), pw);
-        dist = len(lth);
-        ldir = norm(lth);
+        ldir = norm_len(lth, dist);  // dist = len(lth)
       }
     };
 #ifndef RT_LIGHT_SPLIT
