@@ -98,6 +98,24 @@ __device__ __forceinline__ uint64_t num_ok(double n) {
 // form (more scalar branch work). 0: hardware divisions.
 #define RT_FAST_NORM 2
 #endif
+#if RT_FAST_NORM == 2
+// The branch-free half of norm_len: core sqrt and shared-reciprocal quotients,
+// ok = false where a lane must redo them with the hardware sequences
+// (norm_len_fix), so that several normalisations can share one fix-up branch.
+__device__ __forceinline__ d3 norm_len_core(d3 v, double& m, bool& ok) {
+  const double x = v.x * v.x + v.y * v.y + v.z * v.z;
+  m = sqrt_core(x);
+  const double y = rcp_refined(m);
+  const int en = min(min(__builtin_amdgcn_frexp_exp(v.x), __builtin_amdgcn_frexp_exp(v.y)),
+                     __builtin_amdgcn_frexp_exp(v.z));
+  ok = ((uint32_t)__double2hiint(x) - 0x33700000u < 0x18E00000u) & (en > -800);
+  return mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
+}
+__device__ __forceinline__ d3 norm_len_fix(d3 v, double& m) {
+  m = __builtin_sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+  return mk(v.x / m, v.y / m, v.z / m);
+}
+#endif
 // norm(v) that also hands back |v| (the same bits as len(v)).
 __device__ __forceinline__ d3 norm_len(d3 v, double& m) {                                        // vec.go:78,95
 #if RT_FAST_NORM == 2
@@ -108,17 +126,9 @@ __device__ __forceinline__ d3 norm_len(d3 v, double& m) {                       
   // correctly rounded and monotone; 2^198 keeps a round-up to 2^100 out).
   // Numerators: +-0 or |n| >= 2^-800 <=> frexp exponent >= -799 (a zero's
   // exponent is 0, a denormal's < -1021; inf/NaN components fail on x).
-  const double x = v.x * v.x + v.y * v.y + v.z * v.z;
-  m = sqrt_core(x);
-  const double y = rcp_refined(m);
-  d3 r = mk(div_rcp(v.x, m, y), div_rcp(v.y, m, y), div_rcp(v.z, m, y));
-  const int en = min(min(__builtin_amdgcn_frexp_exp(v.x), __builtin_amdgcn_frexp_exp(v.y)),
-                     __builtin_amdgcn_frexp_exp(v.z));
-  const bool ok = ((uint32_t)__double2hiint(x) - 0x33700000u < 0x18E00000u) & (en > -800);
-  if (__builtin_expect(!ok, 0)) {
-    m = __builtin_sqrt(x);
-    r = mk(v.x / m, v.y / m, v.z / m);
-  }
+  bool ok;
+  d3 r = norm_len_core(v, m, ok);
+  if (__builtin_expect(!ok, 0)) r = norm_len_fix(v, m);
   return r;
 #else
   m = gsqrt(v.x * v.x + v.y * v.y + v.z * v.z);
