@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """Benchmark of the render hot path (BASELINE.json metric: Mrays/s at 4K depth 6).
 
-One step = one full frame of the workload per rank (default --scaling weak:
-a batch of N frames, one per GPU, no data-path collective), or one frame with
-its rows sharded across the N ranks and gathered to rank 0 over RCCL
-(--scaling strong). One process per GPU. N=1 workload = config C3 (3840x2160,
-depth 6, cylinder + cube + sphere-for-cone, 4 lights).
+One step = one frame of the workload with its 8-row tile rows dealt
+round-robin across the N ranks and gathered to rank 0 over RCCL (default
+--scaling strong --shard interleaved: BASELINE.json north_star's "image rows
+shard across the GPUs with a final RCCL gather"; at N=1 the single rank
+renders the whole frame and nothing is exchanged), or, with --scaling weak, a
+batch of N frames, one per GPU, with no data-path collective. One process per
+GPU. Workload = config C3 (3840x2160, depth 6, cylinder + cube +
+sphere-for-cone, 4 lights).
 
 Rays = primary + secondary + shadow, counted on the device with the same rule
 as the CPU oracle (include/rt_abi.h rt_stats). value = rays of all ranks per
@@ -41,9 +44,9 @@ def parse():
     p.add_argument("--height", type=int, default=None)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=8)
-    p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                   help="weak: every rank renders its own full frame (no collective); "
-                        "strong: one frame's rows sharded over the ranks + gather")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                   help="strong (default): one frame's rows sharded over the ranks + RCCL gather to "
+                        "rank 0; weak: every rank renders its own full frame (no collective)")
     p.add_argument("--shard", choices=["interleaved", "bands"], default="interleaved",
                    help="row partition for --scaling strong")
     p.add_argument("--accel", choices=["bvh", "none"], default="bvh",
@@ -66,7 +69,32 @@ def pmc_traffic(config):
     return d.get("traffic_bytes"), os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(packed, threads, budget_s=10.0):
+def host_cpu():
+    """(model name, logical CPUs of the machine, CPUs this process may use).
+    On the GPU box nproc / os.cpu_count() count the whole machine; the job's
+    share is its affinity mask, further capped by OMP_NUM_THREADS when set
+    (16 per GPU there)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    ncpu = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = ncpu
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        avail = min(avail, int(omp))
+    return model, ncpu, avail
+
+
+def cpu_sample(packed, threads, budget_s):
     """The CPU oracle (C restatement of the Go path) on this host, `threads`
     workers over (column, 20-row) strips like raytracer.go:611-677, on a
     bounded sample: a band of rows around the middle of the frame, doubled
@@ -88,8 +116,21 @@ def cpu_baseline(packed, threads, budget_s=10.0):
     rays = st.total_rays()
     what = "full %dx%d frame" % (packed.width, H) if (y0 == 0 and y1 == H) else \
         "rows %d..%d of the %dx%d frame" % (y0, y1, packed.width, H)
-    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": "%s of the same scene (%d rays, %.2f s wall)" % (what, rays, dt)}
+    return rays / dt / 1e6, "%s of the same scene (%d rays, %.2f s wall)" % (what, rays, dt)
+
+
+def cpu_baseline(packed, threads, budget_s=10.0):
+    """cpu_baseline: `value` with the reference's fixed 8 render workers
+    (raytracer.go:725 numRenderThreads) and an extra run on every CPU this job
+    may use; oracle built -O3 -ffp-contract=off (oracle/Makefile)."""
+    model, ncpu, avail = host_cpu()
+    v, sample = cpu_sample(packed, threads, budget_s)
+    out = {"value": v, "unit": "Mrays/s", "cores": threads, "kind": "port", "sample": sample,
+           "cpu_model": model, "nproc": ncpu, "cpus_available": avail}
+    if avail != threads:
+        va, sa = cpu_sample(packed, avail, budget_s)
+        out["all_cores"] = {"value": va, "cores": avail, "sample": sa}
+    return out
 
 
 def main():

@@ -203,11 +203,70 @@ __device__ __forceinline__ bool go_is_odd_int(double x) {
   return xf == 0 && ((long long)xi & 1) == 1;
 }
 
+// math.Exp: Go exp.go `exp` + `expmulti` (the portable FreeBSD-derived
+// algorithm): k = int(Log2e*x +- 0.5), r = hi - lo with hi = x - k*Ln2Hi,
+// lo = k*Ln2Lo, a degree-5 rational for e^r, Ldexp. Op for op the oracle's
+// go_exp (oracle/go_math.h), so a fractional Pow is bit-identical on both
+// sides. (Go on amd64 runs exp_amd64.s instead, a CPU-dependent FMA/no-FMA
+// series: the reference's own fractional Pow is not reproducible across
+// CPUs, and no reference fixture exercises it)
+__device__ __noinline__ double go_exp(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double Log2e = 1.44269504088896338700e+00;
+  const double P1 = 1.66666666666666657415e-01, P2 = -2.77777777770155933842e-03,
+               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+               P5 = 4.13813679705723846039e-08;
+  if (__builtin_isnan(x) || x == __builtin_inf()) return x;
+  if (x == -__builtin_inf()) return 0;
+  if (x > 7.09782712893383973096e+02) return __builtin_inf();
+  if (x < -7.45133219101941108420e+02) return 0;
+  if (-3.725290298461914e-09 < x && x < 3.725290298461914e-09) return 1 + x;  // |x| < 2^-28
+  long long k = 0;
+  if (x < 0)
+    k = (long long)(Log2e * x - 0.5);
+  else if (x > 0)
+    k = (long long)(Log2e * x + 0.5);
+  const double hi = x - (double)k * Ln2Hi;
+  const double lo = (double)k * Ln2Lo;
+  const double r = hi - lo;
+  const double t = r * r;
+  const double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+  const double y = 1 - ((lo - (r * c) / (2 - c)) - hi);
+  return ldexp(y, (int)k);
+}
+
+// math.Log: Go log.go `log` (FreeBSD e_log.c), op for op the oracle's go_log.
+__device__ __noinline__ double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (__builtin_isnan(x) || x == __builtin_inf()) return x;
+  if (x < 0) return __builtin_nan("");
+  if (x == 0) return -__builtin_inf();
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < 0.70710678118654752440) {  // Sqrt2/2
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1;
+  const double k = (double)ki;
+  const double s = f / (2 + f);
+  const double s2 = s * s;
+  const double s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2;
+  const double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
 // math.Pow (Go pow.go): special cases, then Frexp + repeated squaring with
 // mantissa renormalisation and a final Ldexp. Integer exponents (the
 // reference's specular n and Schlick's 5) are reproduced exactly; the
-// fractional part goes through exp/log, whose Go amd64 assembly is not
-// restated (parity for fractional specular exponents is unpinned).
+// fractional part is go_exp(yf * go_log(x)), restated identically here and in
+// the oracle.
 __device__ __noinline__ double go_pow_general(double x, double y) {
   if (y == 0 || x == 1) return 1;
   if (y == 1) return x;
@@ -248,7 +307,7 @@ __device__ __noinline__ double go_pow_general(double x, double y) {
       yf--;
       yi++;
     }
-    a1 = exp(yf * log(x));
+    a1 = go_exp(yf * go_log(x));
   }
   int xe;
   double x1 = frexp(x, &xe);

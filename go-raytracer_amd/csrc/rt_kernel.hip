@@ -820,6 +820,16 @@ int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile
   return rc;
 }
 
+int rt_scene_info(rt_context* c, int* flags) {
+  if (!c || !flags) return fail(RT_E_INVALID, "rt_scene_info: NULL argument");
+  if (!c->has_scene) return fail(RT_E_INVALID, "rt_scene_info: no scene set");
+  const DevScene& s = c->sc;
+  const bool lds = scene_in_lds(s);
+  *flags = (lds ? RT_INFO_LDS : 0) | (s.use_bvh ? RT_INFO_BVH : 0) | (s.has_csg ? RT_INFO_CSG : 0) |
+           ((!lds && !s.use_bvh && !s.has_csg) ? RT_INFO_STREAM : 0);
+  return RT_OK;
+}
+
 int rt_specialized(rt_context* c, int* active, double* compile_ms) {
   if (!c) return fail(RT_E_INVALID, "rt_specialized: NULL context");
   if (active) *active = c->spec_fn != nullptr;

@@ -855,6 +855,9 @@ enum VmOp {
   VM_CLAMPF, VM_CLAMPI, VM_TBL, VM_AND, VM_OR, VM_NOT, VM_ERR, VM_RET
 };
 enum { VM_REGS = 64, VM_MAX_STEPS = 8192 };
+static_assert(VM_CONST == RT_VM_CONST && VM_SEL == RT_VM_SEL && VM_TBL == RT_VM_TBL && VM_ERR == RT_VM_ERR &&
+                  VM_RET == RT_VM_RET,
+              "surface bytecode opcodes of include/rt_abi.h");
 
 // Inlined: as an out-of-line call reading the LDS-staged program through
 // generic pointers it rendered wrong pixels on gfx950 (measured: the global

@@ -1,12 +1,12 @@
 """Multi-GPU rendering, one process per GPU.
 
-Weak scaling (bench default, mode "frame"): a batch of frames, one per rank
+Weak scaling (mode "frame", bench --scaling weak): a batch of frames, one per rank
 (e.g. the frames of an animation or of independent requests); each rank renders
 its whole frame into its own HBM buffer. The units (frames, and within them
 pixels) are independent, so there is no data-path collective at all.
 
-Strong scaling (one frame sharded across GPUs + gather to rank 0, RCCL over
-xGMI): pixels are independent and the jitter RNG depends only on (column,
+Strong scaling (the bench default, north_star's design: one frame sharded
+across GPUs + gather to rank 0, RCCL over xGMI): pixels are independent and the jitter RNG depends only on (column,
 20-row strip) (raytracer.go:627-634), so any row partition renders
 bit-identical rows. Two partitions:
 
@@ -51,14 +51,18 @@ def deinterleave(slabs, height):
 _recv = {}
 
 
-def gather_frame(buf, height, mode="bands", group=None):
+def gather_frame(buf, height, mode="bands", group=None, collective=None):
     """Gather every rank's buffer to rank 0 and assemble the [H, W, 4] frame
     there (None elsewhere). Rank 0 receives straight into the slices of one
-    reused [world, ...] tensor (no stacking copy)."""
+    reused [world, ...] tensor (no stacking copy). With a single rank the
+    buffer already is the frame and no collective runs, unless `collective`
+    is True (tests: the RCCL gather at world size 1)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world == 1:
+    if collective is None:
+        collective = world > 1
+    if not collective or not dist.is_initialized():
         return deinterleave(buf.unsqueeze(0), height) if mode == "interleaved" else buf[:height]
     rank = dist.get_rank(group)
     if rank == 0:
@@ -120,7 +124,7 @@ class DistributedRenderer:
             return True
         return self.ntrows > 0 if self.mode == "interleaved" else self.y1 > self.y0
 
-    def step(self, gather=True, events=None):
+    def step(self, gather=True, events=None, collective=None):
         """Render this rank's rows and gather the frame. `events` (start, end):
         torch.cuda.Events recorded on the launch stream around the render
         kernel, for kernel timing without a host sync per step."""
@@ -141,5 +145,5 @@ class DistributedRenderer:
         if events is not None:
             events[1].record()
         if gather:
-            self.frame = gather_frame(self.buf, self.H, self.mode)
+            self.frame = gather_frame(self.buf, self.H, self.mode, collective=collective)
         return self.frame

@@ -63,6 +63,8 @@ def load_library(path=None):
     l.rt_set_specialize.restype = i
     l.rt_set_accel.argtypes = [vp, i]
     l.rt_set_accel.restype = i
+    l.rt_scene_info.argtypes = [vp, C.POINTER(i)]
+    l.rt_scene_info.restype = i
     l.rt_specialized.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
     l.rt_specialized.restype = i
     l.rt_spec_precompile.argtypes = [i, C.POINTER(i), i, C.POINTER(C.c_double)]
@@ -133,6 +135,13 @@ class RenderContext:
         identical pixels and counters). The BVH choice applies at the next
         set_scene; culling applies to specialised kernels."""
         _check(self.lib.rt_set_accel(self.handle, int(flags)), "rt_set_accel")
+
+    def scene_info(self):
+        """rt_scene_info flags of the current scene (abi.RT_INFO_*): which
+        kernel flavour renders it."""
+        f = C.c_int()
+        _check(self.lib.rt_scene_info(self.handle, C.byref(f)), "rt_scene_info")
+        return f.value
 
     def specialized(self):
         """(active, compile_ms): whether the current scene runs a specialised

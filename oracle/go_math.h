@@ -9,6 +9,8 @@
  * published algorithms:
  *   math.Max / math.Min        (dim.go; amd64 assembly has the same semantics)
  *   math.Pow                   (pow.go: Frexp + repeated squaring, Ldexp)
+ *   math.Exp / math.Log        (exp.go, log.go: the portable FreeBSD-derived
+ *                               algorithms; used by Pow's fractional part)
  *   math.Tan / math.Sin / Cos  (tan.go, sin.go: Cephes, Cody-Waite reduction)
  *   math/rand/v2 PCG + Float64 (pcg.go: 128-bit LCG, DXSM output;
  *                               rand.go: Float64 = (u<<11>>11) / 2^53)
@@ -76,10 +78,76 @@ static inline int go_is_odd_int(double x) {
  * identical to C ldexp for every finite input. */
 static inline double go_ldexp(double frac, int e) { return ldexp(frac, e); }
 
-/* Fractional part of Pow needs Exp/Log. The reference scenes only use
- * integer exponents (specular n, Schlick 5); for a fractional exponent we use
- * libm exp/log, which is NOT guaranteed bit-identical to Go's amd64 assembly
- * Exp/Log -- parity for fractional specular exponents is unpinned. */
+/* math.Exp, Go exp.go `exp` (the portable algorithm): argument reduction
+ * x = k*ln2 + r with r = hi - lo, a degree-5 minimax rational for e^r
+ * (expmulti), then Ldexp. The same restatement is rt_device.h go_exp, so HIP
+ * and oracle agree bit for bit. NOTE: on amd64 Go dispatches Exp to assembly
+ * (exp_amd64.s, a different series that uses FMA when the CPU has it), so
+ * the reference's own Exp is CPU-dependent; no reference fixture exercises a
+ * fractional Pow (parity for it is pinned to this restatement only). */
+static inline double go_exp(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01; /* 3fe62e42 fee00000 */
+    const double Ln2Lo = 1.90821492927058770002e-10; /* 3dea39ef 35793c76 */
+    const double Log2e = 1.44269504088896338700e+00;
+    const double Overflow = 7.09782712893383973096e+02;
+    const double Underflow = -7.45133219101941108420e+02;
+    const double NearZero = 1.0 / (1 << 28);
+    const double P1 = 1.66666666666666657415e-01;  /* 3FC55555 55555555 */
+    const double P2 = -2.77777777770155933842e-03; /* BF66C16C 16BEBD93 */
+    const double P3 = 6.61375632143793436117e-05;  /* 3F11566A AF25DE2C */
+    const double P4 = -1.65339022054652515390e-06; /* BEBBBD41 C5D26BF1 */
+    const double P5 = 4.13813679705723846039e-08;  /* 3E663769 72BEA4D0 */
+    if (isnan(x) || (isinf(x) && x > 0)) return x;
+    if (isinf(x)) return 0;
+    if (x > Overflow) return INFINITY;
+    if (x < Underflow) return 0;
+    if (-NearZero < x && x < NearZero) return 1 + x;
+    int64_t k = 0;
+    if (x < 0) k = (int64_t)(Log2e * x - 0.5);
+    else if (x > 0) k = (int64_t)(Log2e * x + 0.5);
+    double hi = x - (double)k * Ln2Hi;
+    double lo = (double)k * Ln2Lo;
+    /* expmulti(hi, lo, k) */
+    double r = hi - lo;
+    double t = r * r;
+    double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    double y = 1 - ((lo - (r * c) / (2 - c)) - hi);
+    return ldexp(y, (int)k);
+}
+
+/* math.Log, Go log.go `log` (FreeBSD e_log.c): Frexp reduction to
+ * f1 in [sqrt(2)/2, sqrt(2)), s = f/(2+f), Remez polynomial in s^2. amd64 Go
+ * has log_amd64.s for the same algorithm; restated from log.go. */
+static inline double go_log(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01; /* 3fe62e42 fee00000 */
+    const double Ln2Lo = 1.90821492927058770002e-10; /* 3dea39ef 35793c76 */
+    const double L1 = 6.666666666666735130e-01;      /* 3FE55555 55555593 */
+    const double L2 = 3.999999999940941908e-01;      /* 3FD99999 9997FA04 */
+    const double L3 = 2.857142874366239149e-01;      /* 3FD24924 94229359 */
+    const double L4 = 2.222219843214978396e-01;      /* 3FCC71C5 1D8E78AF */
+    const double L5 = 1.818357216161805012e-01;      /* 3FC74664 96CB03DE */
+    const double L6 = 1.531383769920937332e-01;      /* 3FC39A09 D078C69F */
+    const double L7 = 1.479819860511658591e-01;      /* 3FC2F112 DF3E5244 */
+    if (isnan(x) || (isinf(x) && x > 0)) return x;
+    if (x < 0) return NAN;
+    if (x == 0) return -INFINITY;
+    int ki;
+    double f1 = go_frexp(x, &ki);
+    if (f1 < 0.70710678118654752440 /* Sqrt2/2 */) { f1 *= 2; ki--; }
+    double f = f1 - 1;
+    double k = (double)ki;
+    double s = f / (2 + f);
+    double s2 = s * s;
+    double s4 = s2 * s2;
+    double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+    double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+    double R = t1 + t2;
+    double hfsq = 0.5 * f * f;
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+/* math.Pow (pow.go). Integer exponents (specular n, Schlick 5) run the
+ * Frexp/squaring loop; a fractional part goes through go_exp(yf*go_log(x)). */
 static inline double go_pow(double x, double y) {
     if (y == 0 || x == 1) return 1;
     if (y == 1) return x;
@@ -119,7 +187,7 @@ static inline double go_pow(double x, double y) {
     int ae = 0;
     if (yf != 0) {
         if (yf > 0.5) { yf--; yi++; }
-        a1 = exp(yf * log(x));
+        a1 = go_exp(yf * go_log(x));
     }
     int xe;
     double x1 = go_frexp(x, &xe);

@@ -925,6 +925,8 @@ int oracle_surface_normal(const rt_scene *in, int idx, int face, const double po
 
 /* Go math restatements exposed for tests. */
 double oracle_go_pow(double x, double y) { return go_pow(x, y); }
+double oracle_go_exp(double x) { return go_exp(x); }
+double oracle_go_log(double x) { return go_log(x); }
 double oracle_go_acos(double x) { return go_acos(x); }
 double oracle_go_atan2(double y, double x) { return go_atan2(y, x); }
 double oracle_go_tan(double x) { return go_tan(x); }

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Generates the reduced-size golden images of the BASELINE configs
+(tests/golden/synthetic/): each rendered by the CPU oracle (oracle/, pinned
+byte-for-byte against the reference's own goldens, tests/test_oracle.py) and
+stored as RGB8 PNG plus the oracle's work counters. Test infrastructure:
+re-run after changing a config; the tests check both the oracle and the HIP
+path against these bytes.
+
+    python tests/golden/make_synthetic.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+from PIL import Image
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+# name -> (config, width, height, row band or None)
+CASES = {
+    "c1_256x256": ("c1", 256, 256, None),
+    "c2_320x180": ("c2", 320, 180, None),
+    "c3_320x180": ("c3", 320, 180, None),
+    "c3cone_320x180": ("c3cone", 320, 180, None),
+    "c4_192x108": ("c4", 192, 108, None),
+    "c4csg_128x72": ("c4csg", 128, 72, None),
+    "c5_96x60_rows20-40": ("c5", 96, 60, (20, 40)),
+}
+
+
+def render(name):
+    from __graft_entry__ import load_package
+    import oracle_bind
+    pkg = load_package()
+    cfg, w, h, band = CASES[name]
+    packed = pkg.scene.convert(pkg.configs.CONFIGS[cfg](width=w, height=h))
+    y0, y1 = band if band else (0, h)
+    img, st = oracle_bind.render_rows(packed, y0, y1)
+    return packed, (y0, y1), img, st
+
+
+def main():
+    out = os.path.join(HERE, "synthetic")
+    os.makedirs(out, exist_ok=True)
+    meta = {}
+    for name in CASES:
+        _, (y0, y1), img, st = render(name)
+        assert (img[..., 3] == 255).all()
+        Image.fromarray(np.ascontiguousarray(img[..., :3])).save(os.path.join(out, name + ".png"), optimize=True)
+        meta[name] = {"config": CASES[name][0], "width": CASES[name][1], "height": CASES[name][2],
+                      "rows": [y0, y1], "stats": st.as_dict()}
+        print(name, st.total_rays(), "rays", flush=True)
+    with open(os.path.join(out, "counters.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -38,7 +38,7 @@ def lib():
         for fn in ("oracle_go_pow",):
             getattr(l, fn).argtypes = [C.c_double, C.c_double]
             getattr(l, fn).restype = C.c_double
-        for fn in ("oracle_go_tan", "oracle_go_sin", "oracle_go_cos"):
+        for fn in ("oracle_go_tan", "oracle_go_sin", "oracle_go_cos", "oracle_go_exp", "oracle_go_log"):
             getattr(l, fn).argtypes = [C.c_double]
             getattr(l, fn).restype = C.c_double
         l.oracle_pcg_float64.argtypes = [C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double)]

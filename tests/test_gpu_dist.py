@@ -1,0 +1,61 @@
+"""The bench's multi-GPU path on a real device: a `nccl` (RCCL) process group
+at world size 1, DistributedRenderer in the strong-scaling modes, the frame
+assembled through the RCCL gather (forced at world size 1) equal to a
+single-context full-frame render. World sizes > 1 need one GPU per rank
+(RCCL rejects two ranks on one device); they are covered with gloo on the CPU
+(tests/test_dist.py) and run by the driver's 8-GPU bench."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import go_raytracer_amd as rt
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def nccl_group():
+    import torch
+    import torch.distributed as dist
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    yield dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["interleaved", "bands", "frame"])
+def test_rccl_gathered_frame_equals_full_render(nccl_group, mode):
+    import torch
+    packed = rt.scene.convert(rt.configs.c3(width=320, height=180))
+    ctx = rt.RenderContext(0)
+    try:
+        ctx.set_scene(packed)
+        full = ctx.render()
+        dr = rt.dist.DistributedRenderer(ctx, packed, 0, 1, torch.device("cuda", 0), mode=mode)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        frame = dr.step(events=ev, collective=True)
+        torch.cuda.synchronize()
+        assert ev[0].elapsed_time(ev[1]) > 0
+        got = frame.cpu().numpy()
+        assert got.shape == full.shape
+        assert np.array_equal(got, full)
+    finally:
+        ctx.close()
+
+
+def test_rccl_max_sum_reduction(nccl_group):
+    import torch
+    mx, sm = rt.dist.reduce_max_sum([1.5, 7.0], device=torch.device("cuda", 0))
+    assert mx == [1.5, 7.0] and sm == [1.5, 7.0]

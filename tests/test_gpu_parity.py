@@ -55,7 +55,8 @@ def test_canned_matches_reference_golden(ctx):
 
 
 @pytest.mark.parametrize("name,w,h", [
-    ("c1", 256, 256), ("c2", 320, 180), ("c3", 320, 180), ("c4", 192, 108), ("canned", 190, 120),
+    ("c1", 256, 256), ("c2", 320, 180), ("c3", 320, 180), ("c3cone", 320, 180), ("c4", 192, 108),
+    ("canned", 190, 120),
 ])
 def test_configs_match_oracle(ctx, name, w, h):
     packed = rt.scene.convert(rt.configs.CONFIGS[name](width=w, height=h))
@@ -479,7 +480,7 @@ def spec_ctx():
 
 
 def _spec_case(case):
-    if case in ("c1", "c2", "c3", "canned"):
+    if case in ("c1", "c2", "c3", "c3cone", "canned"):
         return rt.configs.CONFIGS[case](width=160, height=96)
     if case == "mixed":
         return _mixed_scene(1, 5, 96, 64)
@@ -490,7 +491,7 @@ def _spec_case(case):
     return args
 
 
-@pytest.mark.parametrize("case", ["c1", "c2", "c3", "canned", "mixed", "ext", "sphere", "cube"])
+@pytest.mark.parametrize("case", ["c1", "c2", "c3", "c3cone", "canned", "mixed", "ext", "sphere", "cube"])
 def test_specialised_kernel_matches_oracle(spec_ctx, case):
     packed = rt.scene.convert(_spec_case(case))
     assert packed.scene.num_objects <= 8
@@ -571,3 +572,83 @@ def test_brute_force_search_matches_oracle(case, spec_ctx):
     img2, st2 = render(spec_ctx, packed)
     assert np.array_equal(img, img2)
     assert st.as_dict() == st2.as_dict()
+
+
+# --- the streamed linear search (global scene too large for the LDS copy, no
+# BVH: rt_set_accel(0)) -- BASELINE config 5's regime -- against the oracle.
+
+def _brute(ctx, packed, y0=0, y1=None):
+    try:
+        ctx.set_accel(0)
+        img, st = render(ctx, packed, y0, y1)
+        info = ctx.scene_info()
+    finally:
+        ctx.set_accel(rt.abi.RT_ACCEL_BVH | rt.abi.RT_ACCEL_CULL)
+    return img, st, info
+
+
+@pytest.mark.parametrize("seed,n", [(5, 150), (6, 240)])
+def test_streamed_brute_force_mixed_scene_matches_oracle(ctx, spec_ctx, seed, n):
+    """>= 150 mixed objects (spheres, cubes, cylinders, two planes, exact t
+    ties): far beyond RT_LDS_MAX, so object records stream through the
+    per-wave LDS chunks; generic and specialised kernels, bytes + counters."""
+    packed = rt.scene.convert(_mixed_scene(seed, n, 96, 64))
+    ref, ost = oracle_bind.render_rows(packed)
+    for c in (ctx, spec_ctx):
+        img, st, info = _brute(c, packed)
+        assert info & (rt.abi.RT_INFO_STREAM | rt.abi.RT_INFO_WAVEFRONT), info
+        assert not info & (rt.abi.RT_INFO_LDS | rt.abi.RT_INFO_BVH), info
+        assert_same(img, ref, "streamed mixed seed %d n %d" % (seed, n))
+        assert st.as_dict() == ost.as_dict()
+
+
+def test_streamed_brute_force_c5_band_matches_oracle(ctx):
+    """C5 as BASELINE states it (100k spheres + plane, no BVH): a 20-row band
+    of a 96-pixel-wide frame, every ray against every object in FP64."""
+    packed = rt.scene.convert(rt.configs.c5(width=96, height=60))
+    img, st, info = _brute(ctx, packed, 20, 40)
+    assert info & (rt.abi.RT_INFO_STREAM | rt.abi.RT_INFO_WAVEFRONT), info
+    ref, ost = oracle_bind.render_rows(packed, 20, 40)
+    assert_same(img, ref, "brute-force c5 band")
+    assert st.as_dict() == ost.as_dict()
+    assert st.tests[rt.abi.RT_SPHERE] == 100000 * (st.primary_rays + st.secondary_rays)
+
+
+# --- math.Pow with fractional exponents (Go exp.go / log.go restated on both
+# sides): specular exponents and spot-light falloff.
+
+def test_device_exp_log_pow_equal_oracle_restatement():
+    """tests/hip/pow_check: device go_exp / go_log / go_pow vs the oracle's
+    host restatements, 4M random + edge inputs, bit for bit."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "hip", "pow_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(exe)], check=True)
+    r = subprocess.run([exe, str(1 << 22)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    stats = json.loads(r.stdout.strip().splitlines()[-1])
+    assert stats["pow_mismatches"] == 0 and stats["exp_mismatches"] == 0 and stats["log_mismatches"] == 0
+    assert stats["fractional"] > 0.4 * stats["cases"], stats
+
+
+def _fractional_scene(width, height, exps=(0.5, 2.5, 7.3, 33.3), spot_exp=2.7):
+    mats = [S.material((0.8, 0.3 + 0.1 * i, 0.2), 0.2 * (i % 2), 0.0, 0.0, 0.0, 0.9, 0.7, n)
+            for i, n in enumerate(exps)]
+    objs = [S.Sphere(m).translate(-2.4 + 1.6 * i, 0.0, 6.0) for i, m in enumerate(mats)]
+    objs.append(S.Plane(S.material((0.6, 0.6, 0.6), 0.2, 0.0, 0.0, 0.0, 1.0, 0.5, 12.5)).translate(0.0, -1.0, 0.0))
+    lights = [S.PointLight((4.0, 5.0, 0.0), (0.7, 0.7, 0.7)),
+              S.SpotLight((0.0, 6.0, 3.0), (0.0, -1.0, 6.0), (0.6, 0.6, 0.5), 40.0, spot_exp)]
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=S.Union(tuple(objs)), depth=3, fov=80.0,
+                        width=width, height=height, bg_start=(0.0, 0.0, 0.0), bg_end=(0.5, 0.7, 1.0))
+
+
+def test_fractional_specular_and_spot_exponents_match_oracle(ctx, spec_ctx):
+    """n in {0.5, 2.5, 7.3, 33.3} (specular) and a 2.7 spot falloff: the
+    fractional branch of math.Pow on the device equals the oracle's."""
+    packed = rt.scene.convert(_fractional_scene(160, 96))
+    ref, ost = oracle_bind.render_rows(packed)
+    for c in (ctx, spec_ctx):
+        img, st = render(c, packed)
+        assert_same(img, ref, "fractional exponents")
+        assert st.as_dict() == ost.as_dict()

@@ -118,6 +118,46 @@ def test_go_pow_integer_exponents_match_repeated_squaring():
     assert abs(l.oracle_go_pow(x, 50.0) - x ** 50) <= 4e-16
 
 
+def _ulps(a, b):
+    ia = int(np.array(a).view(np.int64))
+    ib = int(np.array(b).view(np.int64))
+    return abs(ia - ib)
+
+
+def test_go_exp_log_restatement():
+    """math.Exp / math.Log (Go exp.go, log.go; the fractional branch of
+    math.Pow): special cases, exact points, and within 1 ulp of libm (both
+    algorithms are < 1 ulp; bit-exactness with the device is tests/hip/pow_check)."""
+    l = oracle_bind.lib()
+    assert l.oracle_go_exp(0.0) == 1.0 and l.oracle_go_log(1.0) == 0.0
+    assert l.oracle_go_exp(float("-inf")) == 0.0 and l.oracle_go_exp(float("inf")) == float("inf")
+    assert l.oracle_go_exp(710.0) == float("inf") and l.oracle_go_exp(-746.0) == 0.0
+    assert math.isnan(l.oracle_go_exp(float("nan"))) and math.isnan(l.oracle_go_log(-1.0))
+    assert l.oracle_go_log(0.0) == float("-inf") and l.oracle_go_log(float("inf")) == float("inf")
+    assert l.oracle_go_exp(1e-9) == 1.0 + 1e-9  # |x| < 2^-28: 1 + x
+    assert l.oracle_go_log(2.0) == 0.6931471805599453 and l.oracle_go_log(0.5) == -0.6931471805599453
+    rng = np.random.default_rng(5)
+    for x in rng.uniform(-700, 700, 20000):
+        assert _ulps(l.oracle_go_exp(x), math.exp(x)) <= 1, x
+    for x in np.exp(rng.uniform(-700, 700, 20000)):
+        assert _ulps(l.oracle_go_log(x), math.log(x)) <= 1, x
+    for x in np.concatenate([rng.uniform(0, 1, 5000), [5e-324, 1e-310, 0.7071067811865476, 1 - 2 ** -53]]):
+        assert _ulps(l.oracle_go_log(x), math.log(x)) <= 1, x
+
+
+@pytest.mark.parametrize("y", [0.5, 2.5, 7.3, 33.3, -1.5, 0.75])
+def test_go_pow_fractional_exponents(y):
+    """Pow's fractional part: yf > 0.5 folds to yf - 1 (yi + 1), then
+    Exp(yf * Log(x)) times the repeated-squaring integer part."""
+    l = oracle_bind.lib()
+    rng = np.random.default_rng(int(y * 100) & 0xffff)
+    for x in rng.uniform(1e-3, 1.0, 3000):
+        got, want = l.oracle_go_pow(x, y), x ** y
+        assert abs(got - want) <= 64 * abs(want) * 2.0 ** -52, (x, y, got, want)  # not correctly rounded
+    assert math.isnan(l.oracle_go_pow(-0.5, y))
+    assert l.oracle_go_pow(1.0, y) == 1.0
+
+
 def test_go_tan_matches_libm_closely():
     l = oracle_bind.lib()
     for deg in (30.0, 45.0, 60.0, 89.0):
