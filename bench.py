@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--accel", choices=["bvh", "none"], default="bvh",
                    help="none: the reference's brute-force search (no BVH, no culling; identical pixels "
                         "and counters) -- BASELINE config 5's regime, the FP64 roofline of the Intersect loop")
+    p.add_argument("--rows", default=None, metavar="Y0:Y1",
+                   help="render only rows [Y0, Y1) of the full-size frame (one GPU): a full-width row "
+                        "band of a config too costly to render whole (brute-force C5 at 7680x4320)")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -67,6 +70,17 @@ def pmc_traffic(config):
     with open(path) as f:
         d = json.load(f)
     return d.get("traffic_bytes"), os.path.relpath(path, ROOT)
+
+
+def pmc_executed(key):
+    """Executed-work counters of the render kernel for this workload from the
+    committed rocprofv3 --pmc summary (profiles/pmc_<key>.json, written by
+    scripts/pmc_roofline.py from passes over the same kernel build)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % key)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        return json.load(f), os.path.relpath(path, ROOT)
 
 
 def host_cpu():
@@ -163,7 +177,13 @@ def main():
     ctx.set_scene(packed)
     spec_active, spec_ms = ctx.specialized()
     mode = "frame" if args.scaling == "weak" else args.shard
-    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=mode)
+    band = None
+    if args.rows:
+        if world != 1:
+            raise SystemExit("--rows is a one-GPU measurement")
+        band = tuple(int(v) for v in args.rows.split(":"))
+        mode = "band"
+    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=mode, band=band)
 
     def barrier():
         if world > 1:
@@ -222,7 +242,8 @@ def main():
                        "width": packed.width, "height": packed.height, "depth": rargs.depth,
                        "lights": len(rargs.lights), "objects": int(packed.scene.num_objects),
                        "rays_per_step": int(per_step_rays),
-                       "parallelism": ("frame-per-gpu%d" % world) if args.scaling == "weak"
+                       "parallelism": ("rows %d:%d (band)" % band) if band else
+                                      ("frame-per-gpu%d" % world) if args.scaling == "weak"
                                       else "rows%d-%s" % (world, args.shard),
                        "kernel": "specialised" if spec_active else "generic",
                        "accel": "bvh+cull" if args.accel == "bvh" else "none (brute force)",
@@ -235,8 +256,22 @@ def main():
                          "traffic": None, "traffic_source": None},
             "cpu_baseline": None,
         }
+        # What the kernel executes (PMC) next to the reference-algorithmic frac
+        key = args.config + ("_bf" if args.accel == "none" else "") + \
+            ("_rows%d-%d" % band if band else "")
+        ex, exsrc = pmc_executed(key) if (world == 1 and not args.width and not args.height) else (None, None)
+        if ex is not None and kavg > 0:
+            ex_tf = ex["executed_fp64_flops"] / (kavg * 1e-3) / 1e12
+            line["roofline"].update({
+                "executed_tflops": round(ex_tf, 3),
+                "executed_frac": round(ex_tf / PEAK_FP64_TFLOPS, 4),
+                "fp64_pipe_busy": round(ex["fp64_pipe_busy"], 4),
+                "valu_busy": round(ex["valu_busy"], 4),
+                "issue_util": round(ex["issue_util"], 4),
+                "lane_util": round(ex["lane_util"], 4),
+                "pmc_source": exsrc})
         tb, src = pmc_traffic(args.config)
-        if tb is not None and world == 1 and not args.width and not args.height:
+        if tb is not None and world == 1 and not args.width and not args.height and not band:
             line["roofline"]["traffic"] = int(tb)
             line["roofline"]["traffic_source"] = src
         if world == 1 and args.cpu_baseline == "auto":

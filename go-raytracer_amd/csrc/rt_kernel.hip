@@ -240,7 +240,8 @@ struct DevScene {
   int nplanes = 0, nnodes = 0, kind_mask = 0;
   int light_mask = 0;  // bit k: the scene has lights of kind k (RT_LIGHT_*)
   int leaf_kind_mask = 0;  // bit k: some CSG leaf has kind k
-  size_t off_nodes = 0, off_bobj = 0, off_planes = 0;
+  size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0;
+  int nruns = 0;
 };
 
 #ifndef RT_BVH_SAH
@@ -1300,7 +1301,17 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     s.off_nodes = 0;
     s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
     s.off_planes = s.off_bobj + ((b.leaf_geo.size() * sizeof(double) + 15) & ~(size_t)15);
-    std::vector<char> acc(s.off_planes + std::max<size_t>(1, planes.size()) * sizeof(int), 0);
+    // maximal runs of consecutive top-level objects of one kind (brute-force
+    // loops over global linear scenes: first, count, kind, 0)
+    std::vector<int> runs;
+    for (int i = 0; i < s.nobj; i++) {
+      if (runs.empty() || runs[runs.size() - 2] != kind[i]) runs.insert(runs.end(), {i, 0, kind[i], 0});
+      runs[runs.size() - 3]++;
+    }
+    s.nruns = (int)runs.size() / 4;
+    s.off_runs = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
+    std::vector<char> acc(s.off_runs + std::max<size_t>(1, runs.size()) * sizeof(int), 0);
+    if (!runs.empty()) std::memcpy(acc.data() + s.off_runs, runs.data(), runs.size() * sizeof(int));
     if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
     if (!b.leaf_geo.empty())
       std::memcpy(acc.data() + s.off_bobj, b.leaf_geo.data(), b.leaf_geo.size() * sizeof(double));
@@ -1362,7 +1373,11 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int jump_off = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
   // per-wave object-record stream buffers (global linear scenes, RT_STREAM)
   const int stream_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);
-  const bool use_stream = !lds && !s.use_bvh && !s.has_csg;
+  // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
+  // loads instead: no stream buffers)
+  // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)
+  static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
+  const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
   const void* kfn;
@@ -1453,6 +1468,8 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.frames = std::max(1, s.depth - 1);
   P.kind_mask = s.kind_mask;
   P.cnt_off = cnt_off;
+  P.runs = reinterpret_cast<const int*>(s.accel + s.off_runs);
+  P.nruns = s.nruns;
   if (s.use_bvh) {
     P.bvh_nodes = reinterpret_cast<const float*>(s.accel + s.off_nodes);
     P.bvh_geo = reinterpret_cast<const double*>(s.accel + s.off_bobj);

@@ -46,6 +46,12 @@
 #ifndef RT_STREAM
 #define RT_STREAM 1  // global linear scenes: object records stream through per-wave LDS buffers
 #endif
+#ifndef RT_STREAM_SMEM
+#define RT_STREAM_SMEM 1  // ... or, in the brute-force build (RT_CULL=0), through scalar loads in kind runs
+#endif
+#ifndef RT_SHADOW_CHECK
+#define RT_SHADOW_CHECK 8  // brute-force shadow runs: wave-level "any ray open?" test every N objects
+#endif
 #ifndef RT_BRANCHFREE
 #define RT_BRANCHFREE 0  // straight-line Intersect routines: measured -35M scalar, +45M vector instructions on C3, no faster
 #endif
@@ -143,6 +149,10 @@ struct Params {
   const double* bvh_geo;   // leaf objects in BVH order: geo record, 14 = index, 15 = kind
   const int* planes;       // unbounded objects, ascending index
   int nplanes, bvh_stack_off;
+  // Global linear scenes: maximal runs of consecutive objects of one kind,
+  // [nruns][4] = first index, count, kind, 0 (brute-force scalar-load loops)
+  const int* runs;
+  int nruns;
   int cnt_off;    // LDS byte offset of the per-lane event counters [NCNT][WG]
   int kind_mask;  // bit k: the scene has objects of kind k
 };
@@ -170,6 +180,51 @@ __device__ __forceinline__ Ray to_obj(const double* m, const Ray& r) {
   l.d = mk(m[0] * r.d.x + m[1] * r.d.y + m[2] * r.d.z, m[4] * r.d.x + m[5] * r.d.y + m[6] * r.d.z,
            m[8] * r.d.x + m[9] * r.d.y + m[10] * r.d.z);
   return l;
+}
+
+// Object records read through the constant address space: a wave-uniform
+// index then compiles to scalar loads (s_load_dwordx16 + x8 for the 12
+// WorldToObject doubles), which land in SGPRs and feed the FP64 VALU ops as
+// their scalar operand -- no LDS or vector-memory bandwidth per object.
+typedef const __attribute__((address_space(4))) double* cdptr;
+struct Rec12 {
+  double m[12];
+};
+__device__ __forceinline__ Rec12 ld_rec12(cdptr p) {
+  Rec12 r;
+#pragma unroll
+  for (int q = 0; q < 12; q++) r.m[q] = p[q];
+  return r;
+}
+// Index of the next record to prefetch, made to depend on the current record
+// (an empty asm that "reads" it): scalar loads return out of order, so the
+// only wait the compiler can emit is lgkmcnt(0); this places that wait before
+// the next record's loads are issued instead of right after them, so they
+// stay in flight while the current record is tested.
+__device__ __forceinline__ cdptr after_rec(cdptr next, const Rec12& cur) {
+  asm volatile("" : "+s"(next) : "s"(cur.m[0]));
+  return next;
+}
+// body(i, rec) for the objects i = r0 .. r0 + rn - 1 in index order, records
+// read with scalar loads, the next record in flight while one is tested. Two
+// register sets alternate (no copies between iterations). With CHECK > 0
+// (even), stop() -- wave-uniform -- is asked every CHECK objects.
+template <int CHECK, typename Body, typename Stop>
+__device__ __forceinline__ void scan_records(cdptr base, int r0, int rn, Body&& body, Stop&& stop) {
+  cdptr p = base + (size_t)r0 * 16;  // GEO doubles per record
+  Rec12 A = ld_rec12(p);
+  int j = 0;
+  for (; j + 2 <= rn; j += 2, p += 2 * 16) {
+    if (CHECK > 0 && j > 0 && (j % CHECK) == 0 && stop()) return;
+    const Rec12 B = ld_rec12(after_rec(p + 16, A));
+    body(r0 + j, A);
+    A = ld_rec12(after_rec(j + 2 < rn ? p + 2 * 16 : p + 16, B));
+    body(r0 + j + 1, B);
+  }
+  if (j < rn) {
+    if (CHECK > 0 && j > 0 && (j % CHECK) == 0 && stop()) return;
+    body(r0 + j, A);
+  }
 }
 
 // True when q = num/den (den != 0, finite) is certainly <= 0, i.e. num == 0
@@ -1342,10 +1397,42 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         }
 #else
         if constexpr (STREAM) {
+#if RT_STREAM_SMEM && !RT_CULL
+          // Brute force over a global linear scene, in kind runs. A sphere run
+          // is a scalar-load loop with the next record in flight: every lane
+          // forms the quadratic (Sphere.Intersect, raytracer.go:58-104) and only
+          // lanes with a real root take the sqrt/division branch; index order,
+          // strict < (closestHit, raytracer.go:469-483).
+          const cdptr cgeo = (cdptr)S.geo;
+          for (int r = 0; r < P.nruns; r++) {
+            const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
+              scan_records<0>(cgeo, r0, rn, [&](int i, const Rec12& R) {
+                const Ray l = to_obj(R.m, ray);
+                const double a = dot(l.d, l.d);
+                const double hb = dot(l.o, l.d);
+                const double c = dot(l.o, l.o) - 1.0;
+                const double disc = hb * hb - a * c;
+                if (tr && !(disc < 0.0)) {
+                  const double t0 = (-hb - gsqrt(disc)) / a;
+                  if (t0 > 0.0 && (!found || t0 < best_t)) {
+                    found = true;
+                    best_t = t0;
+                    best_i = i;
+                    best_f = 0;
+                  }
+                }
+              }, [] { return false; });
+            } else {
+              for (int i = r0; i < r0 + rn; i++) trace_obj(i, rk, S.geo + (size_t)i * GEO, tr);
+            }
+          }
+#else
           stream_objects([&](int i, int k, const double* g) {
             trace_obj(i, k, g, tr);
             return true;
           });
+#endif
         } else {
           for (int i = 0; i < P.nobj; i++) trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
         }
@@ -1633,6 +1720,44 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const int k = spec_kinds[i];
 #else
         if constexpr (STREAM) {
+#if RT_STREAM_SMEM && !RT_CULL
+          // Brute force in kind runs (see the TRACE pass); inShadow stops at the
+          // first occluder (raytracer.go:411-429), the wave once no lane is open
+          // (tested every RT_SHADOW_CHECK objects: a closed lane never reopens).
+          const cdptr cgeo = (cdptr)S.geo;
+          for (int r = 0; r < P.nruns; r++) {
+            if (!__any(open)) break;
+            const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
+              scan_records<RT_SHADOW_CHECK>(cgeo, r0, rn, [&](int i, const Rec12& R) {
+                const Ray l = to_obj(R.m, sr);
+                const double a = dot(l.d, l.d);
+                const double hb = dot(l.o, l.d);
+                const double c = dot(l.o, l.o) - 1.0;
+                const double disc = hb * hb - a * c;
+                if (open && i != hit_i && !(disc < 0.0)) {
+                  const double t0 = (-hb - gsqrt(disc)) / a;
+                  if (t0 > 0.0 && t0 * rlen < dist) {
+                    open = false;
+                    send = i + 1;
+                  }
+                }
+              }, [&] { return !__any(open); });
+            } else {
+              for (int i = r0; i < r0 + rn; i++) {
+                if (!__any(open)) break;
+                if (open && i != hit_i) {
+                  double t;
+                  int f;
+                  if (object_hit(rk, S.geo + (size_t)i * GEO, sr, t, f) && t * rlen < dist) {
+                    open = false;
+                    send = i + 1;
+                  }
+                }
+              }
+            }
+          }
+#else
           stream_objects([&](int i, int k, const double* g) {
             if (!__any(open)) return false;
             bool test = open && i != hit_i;
@@ -1652,6 +1777,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             }
             return true;
           });
+#endif
         }
         for (int i = STREAM ? P.nobj : 0; i < P.nobj; i++) {
           if (!__any(open)) break;

@@ -98,7 +98,7 @@ class DistributedRenderer:
     share of one frame's rows ("interleaved" / "bands", strong scaling) followed
     by the gather to rank 0."""
 
-    def __init__(self, ctx, packed, rank, world, device, mode="interleaved"):
+    def __init__(self, ctx, packed, rank, world, device, mode="interleaved", band=None):
         import torch
         self.ctx = ctx
         self.packed = packed
@@ -109,6 +109,15 @@ class DistributedRenderer:
         self.W = packed.width
         if mode == "frame":
             rows = self.H
+        elif mode == "band":
+            # one fixed row band [y0, y1) of the full-size frame, one rank
+            # (measurement of configs too costly to render whole, e.g. brute-force C5)
+            if world != 1 or band is None:
+                raise ValueError("mode 'band' takes band=(y0, y1) and one rank")
+            self.y0, self.y1 = int(band[0]), int(band[1])
+            if not 0 <= self.y0 < self.y1 <= self.H:
+                raise ValueError("band %r outside the %d-row frame" % (band, self.H))
+            rows = self.y1 - self.y0
         elif mode == "interleaved":
             self.nt, self.K = tile_rows(self.H, world)
             # this rank's valid tile rows (the rest of its slab is padding)
@@ -120,7 +129,7 @@ class DistributedRenderer:
         self.frame = None
 
     def has_work(self):
-        if self.mode == "frame":
+        if self.mode in ("frame", "band"):
             return True
         return self.ntrows > 0 if self.mode == "interleaved" else self.y1 > self.y0
 
@@ -130,11 +139,14 @@ class DistributedRenderer:
         kernel, for kernel timing without a host sync per step."""
         if events is not None:
             events[0].record()
-        if self.mode == "frame":
-            self.ctx.render_rows_async(0, self.H, self.buf)
+        if self.mode in ("frame", "band"):
+            if self.mode == "frame":
+                self.ctx.render_rows_async(0, self.H, self.buf)
+            else:
+                self.ctx.render_rows_async(self.y0, self.y1, self.buf)
             if events is not None:
                 events[1].record()
-            self.frame = self.buf  # rank-local frame; nothing to exchange
+            self.frame = self.buf  # rank-local rows; nothing to exchange
             return self.frame
         if self.mode == "interleaved":
             if self.ntrows > 0:

@@ -1,10 +1,16 @@
-# Brute-force C5 (480x270) under compile-time variants of the streamed loop.
+# A/B of brute-force kernel variants (RT_SPEC_EXTRA_FLAGS) on a full-width C5
+# row band.  usage: bash scripts/gpu_brute_ab.sh ROWS "FLAGS_A" "FLAGS_B" ...
+# (an empty string = the default build)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/brute_ab
-i=0
-for fl in "$@"; do
-  i=$((i+1))
-  RT_SPEC_EXTRA_FLAGS="$fl" timeout -k 10 200 python bench.py --config c5 --width 480 --height 270 --accel none --steps 2 --warmup 1 --cpu-baseline off > gpurun_out/brute_ab/v$i.json 2> gpurun_out/brute_ab/v$i.err || { echo "FAIL v$i"; tail -3 gpurun_out/brute_ab/v$i.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['ms_per_step'], d['roofline']['frac'])" gpurun_out/brute_ab/v$i.json "v$i[$fl]"
+ROWS=$1; shift
+mkdir -p gpurun_out/ab
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "brute or stream" --timeout 300 --timeout-method thread > gpurun_out/pytest_brute.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_brute.log; exit 1; }
+tail -1 gpurun_out/pytest_brute.log
+n=0
+for f in "$@"; do
+  n=$((n+1))
+  if [ -n "$f" ]; then export RT_SPEC_EXTRA_FLAGS="$f"; else unset RT_SPEC_EXTRA_FLAGS; fi
+  timeout -k 10 400 python3 bench.py --config c5 --accel none --rows $ROWS --steps 1 --warmup 1 --cpu-baseline off > gpurun_out/ab/v$n.json 2> gpurun_out/ab/v$n.err || { echo "variant $n failed"; tail -5 gpurun_out/ab/v$n.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/v$n.json')); print('[$f]', d['ms_per_step'], 'ms', d['roofline']['frac'])"
 done

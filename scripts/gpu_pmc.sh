@@ -15,4 +15,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/p3 -o p3 --output-format csv -- $B > /dev/null 2>&1 && \
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d $O/p4 -o p4 --output-format csv -- $B > /dev/null 2>&1 && \
 python3 scripts/pmc_summary.py "$O/p*/*counter_collection.csv" > $O/summary.txt && \
+python3 scripts/pmc_roofline.py "$O/p[12]/*counter_collection.csv" $O/pmc_$CFG.json && \
 python3 scripts/pmc_traffic.py "$O/p[34]/*counter_collection.csv" $O/traffic.json "$O/cal_*/*counter_collection.csv" && cat $O/summary.txt $O/traffic.json

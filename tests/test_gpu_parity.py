@@ -602,16 +602,19 @@ def test_streamed_brute_force_mixed_scene_matches_oracle(ctx, spec_ctx, seed, n)
         assert st.as_dict() == ost.as_dict()
 
 
-def test_streamed_brute_force_c5_band_matches_oracle(ctx):
+def test_streamed_brute_force_c5_band_matches_oracle(ctx, spec_ctx):
     """C5 as BASELINE states it (100k spheres + plane, no BVH): a 20-row band
-    of a 96-pixel-wide frame, every ray against every object in FP64."""
+    of a 96-pixel-wide frame, every ray against every object in FP64 -- the
+    generic kernel (LDS-chunk stream) and the specialised brute-force kernel
+    (scalar-load sphere runs)."""
     packed = rt.scene.convert(rt.configs.c5(width=96, height=60))
-    img, st, info = _brute(ctx, packed, 20, 40)
-    assert info & (rt.abi.RT_INFO_STREAM | rt.abi.RT_INFO_WAVEFRONT), info
     ref, ost = oracle_bind.render_rows(packed, 20, 40)
-    assert_same(img, ref, "brute-force c5 band")
-    assert st.as_dict() == ost.as_dict()
-    assert st.tests[rt.abi.RT_SPHERE] == 100000 * (st.primary_rays + st.secondary_rays)
+    for c in (ctx, spec_ctx):
+        img, st, info = _brute(c, packed, 20, 40)
+        assert info & (rt.abi.RT_INFO_STREAM | rt.abi.RT_INFO_WAVEFRONT), info
+        assert_same(img, ref, "brute-force c5 band")
+        assert st.as_dict() == ost.as_dict()
+        assert st.tests[rt.abi.RT_SPHERE] == 100000 * (st.primary_rays + st.secondary_rays)
 
 
 # --- math.Pow with fractional exponents (Go exp.go / log.go restated on both
