@@ -1421,6 +1421,10 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   }
   const int ext_off = shmem + lds_levels * level_bytes;
   shmem = ext_off + lds_full * ext_bytes;
+  static const bool dbg = getenv("RT_DEBUG_LAUNCH") != nullptr;
+  if (dbg)
+    fprintf(stderr, "[launch] blocks/CU %d, LDS/block %d B (fixed %d, frame cores %d levels, full frames %d levels), frames %d\n",
+            per_cu, shmem, frames_off, lds_levels, lds_full, frames);
   const int grid = c->cus * std::min(per_cu, 8);
   if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
   Params P;
