@@ -49,6 +49,9 @@
 #ifndef RT_STREAM_SMEM
 #define RT_STREAM_SMEM 1  // ... or, in the brute-force build (RT_CULL=0), through scalar loads in kind runs
 #endif
+#ifndef RT_SHADOW_JOINT
+#define RT_SHADOW_JOINT 1  // brute force, specialised light count: one sweep for all shadow rays of a hit
+#endif
 #ifndef RT_SHADOW_CHECK
 #define RT_SHADOW_CHECK 8  // brute-force shadow runs: wave-level "any ray open?" test every N objects
 #endif
@@ -1680,6 +1683,86 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(S.lights + (size_t)li * LGT, ldir_a[li], dist_a[li]);
 #endif
+#if RT_STREAM_SMEM && !RT_CULL && RT_SHADOW_JOINT && !defined(RT_SPEC_NOBJ)
+#define RT_JOINT_SWEEP 1
+#else
+#define RT_JOINT_SWEEP 0
+#endif
+#if RT_JOINT_SWEEP
+    // Brute force over a global linear scene: one sweep over the objects for
+    // every light's shadow ray of this hit (inShadow per light, raytracer.go:
+    // 411-429, each stopping at its own first occluder). The rays share their
+    // origin, so the object-space origin and c = |o|^2 - 1 are formed once per
+    // object -- the same operations as one to_obj + Sphere.Intersect per light
+    // (raytracer.go:51-56, 58-104), so verdicts and counts are bit-identical.
+    bool jopen[RT_SPEC_NLIGHTS];
+    int jsend[RT_SPEC_NLIGHTS];
+#pragma unroll
+    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+      jopen[li] = hit;
+      jsend[li] = P.nobj;
+    }
+    if constexpr (STREAM) {
+      const cdptr cgeo = (cdptr)S.geo;
+      bool lon[RT_SPEC_NLIGHTS];  // wave-uniform: light li still has an open lane
+      auto refresh = [&]() {
+        bool any = false;
+#pragma unroll
+        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+          lon[li] = __any(jopen[li]);
+          any = any || lon[li];
+        }
+        return any;
+      };
+      for (int r = 0; r < P.nruns; r++) {
+        if (!refresh()) break;
+        const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
+        if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
+          scan_records<RT_SHADOW_CHECK>(cgeo, r0, rn, [&](int i, const Rec12& R) {
+            const double* m = R.m;
+            const d3 lo = mk(m[0] * sorig.x + m[1] * sorig.y + m[2] * sorig.z + m[3],
+                             m[4] * sorig.x + m[5] * sorig.y + m[6] * sorig.z + m[7],
+                             m[8] * sorig.x + m[9] * sorig.y + m[10] * sorig.z + m[11]);
+            const double c = dot(lo, lo) - 1.0;
+#pragma unroll
+            for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+              if (!lon[li]) continue;
+              const d3 dw = ldir_a[li];
+              const d3 ld = mk(m[0] * dw.x + m[1] * dw.y + m[2] * dw.z, m[4] * dw.x + m[5] * dw.y + m[6] * dw.z,
+                               m[8] * dw.x + m[9] * dw.y + m[10] * dw.z);
+              const double a = dot(ld, ld);
+              const double hb = dot(lo, ld);
+              const double disc = hb * hb - a * c;
+              if (jopen[li] && i != hit_i && !(disc < 0.0)) {
+                const double t0 = (-hb - gsqrt(disc)) / a;
+                if (t0 > 0.0 && t0 * rlen < dist_a[li]) {
+                  jopen[li] = false;
+                  jsend[li] = i + 1;
+                }
+              }
+            }
+          }, [&] { return !refresh(); });
+        } else {
+          for (int i = r0; i < r0 + rn; i++) {
+#pragma unroll
+            for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+              if (jopen[li] && i != hit_i) {
+                Ray sr;
+                sr.o = sorig;
+                sr.d = ldir_a[li];
+                double t;
+                int f;
+                if (object_hit(rk, S.geo + (size_t)i * GEO, sr, t, f) && t * rlen < dist_a[li]) {
+                  jopen[li] = false;
+                  jsend[li] = i + 1;
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+#endif
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
       const double* lt = S.lights + (size_t)li * LGT;
@@ -1720,7 +1803,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const int k = spec_kinds[i];
 #else
         if constexpr (STREAM) {
-#if RT_STREAM_SMEM && !RT_CULL
+#if defined(RT_SPEC_NLIGHTS) && RT_JOINT_SWEEP
+          open = jopen[li];  // the joint sweep above
+          send = jsend[li];
+#elif RT_STREAM_SMEM && !RT_CULL
           // Brute force in kind runs (see the TRACE pass); inShadow stops at the
           // first occluder (raytracer.go:411-429), the wave once no lane is open
           // (tested every RT_SHADOW_CHECK objects: a closed lane never reopens).
