@@ -428,6 +428,7 @@ int align16(int v) { return (v + 15) & ~15; }
 
 struct rt_context {
   int device = 0;
+  int last_waves = 0, launches = 0;  // diagnostics (RT_PHASE_TIMING wave lifetimes)
   int cus = 0;
   int lds_per_cu = 0, lds_per_block = 0;  // bytes (device properties)
   int grid_lds = 0, grid_glb = 0;  // persistent grids (workgroups) per kernel flavour
@@ -1426,6 +1427,8 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     fprintf(stderr, "[launch] blocks/CU %d, LDS/block %d B (fixed %d, frame cores %d levels, full frames %d levels), frames %d\n",
             per_cu, shmem, frames_off, lds_levels, lds_full, frames);
   const int grid = c->cus * std::min(per_cu, 8);
+  c->last_waves = grid * WAVES_PER_WG;
+  c->launches++;
   if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
   Params P;
   std::memset(&P, 0, sizeof P);
@@ -1565,8 +1568,11 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
       fprintf(stderr, "[phase]");
       for (int k = 0; k < N_PHASE; k++) fprintf(stderr, " %s=%.3f", nm[k], (double)ph[k] / (double)tot);
       fprintf(stderr, " total_wave_cycles=%.4g\n", (double)tot);
-      unsigned long long bd[6];
+      unsigned long long bd[8];
       HIP_TRY(hipMemcpy(bd, c->stats + ST_BVHDIAG, sizeof bd, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[waves] lifetime mean %.4g cycles, max %.4g cycles (mean/max %.3f)\n",
+              (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches), (double)bd[7],
+              (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches) / (double)std::max(1ull, bd[7]));
       if (bd[4] + bd[5])
         fprintf(stderr, "[bvh] wave traversals trace=%llu shadow=%llu; nodes/traversal trace=%.1f shadow=%.1f; "
                         "leaves/traversal trace=%.1f shadow=%.1f\n", bd[4], bd[5], (double)bd[0] / (double)std::max(1ull, bd[4]),
@@ -1588,6 +1594,7 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
     HIP_TRY(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st));
     HIP_TRY(hipStreamSynchronize(st));
     c->primary_pending = 0;
+    c->launches = 0;
   }
   return RT_OK;
 }

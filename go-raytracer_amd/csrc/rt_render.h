@@ -729,9 +729,9 @@ __device__ __forceinline__ bool csg_eval(const int* code, int n, uint64_t m0, ui
 // (strictly beyond, or at-or-beyond when !cut_strict): the caller cannot use
 // such a hit (closest hit: t > best; shadow: t * |d| >= dist), so stopping
 // there changes no result.
-__device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, const int* code, int nobj,
-                                        const double* g, const Ray& r, double& t, int& face, double cut_m = 1.0,
-                                        double cut_lim = __builtin_inf(), bool cut_strict = true) {
+__device__ __forceinline__ bool csg_hit_all(const double* geo, const int* kinds, const int* code, int nobj,
+                                            const double* g, const Ray& r, double& t, int& face, double cut_m,
+                                            double cut_lim, bool cut_strict) {
   const int* ci = reinterpret_cast<const int*>(g + 14);
   const int first = nobj + ci[0], count = ci[1];
   const int* prog = code + ci[2];
@@ -804,6 +804,108 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
       const int flip = ((jend == 0) != after) ? 1 : 0;
       t = te;
       face = (je << 4) | (flip << 3) | (jend ? (F[je] >> 4) & 15 : F[je] & 15);
+      return true;
+    }
+    tc = te;
+  }
+}
+
+// The same search over a register-resident list of the live leaves (at most
+// RT_CSG_LIVE per lane, ascending leaf order, so every tie breaks as above):
+// a ray meets only a few of a composite's leaves, and the per-lane interval
+// arrays of csg_hit_all live in scratch memory. A lane with more live leaves
+// redoes the search with csg_hit_all (identical result).
+#ifndef RT_CSG_LIVE
+#define RT_CSG_LIVE 6  // 0: always the scratch-array search
+#endif
+__device__ __forceinline__ bool csg_hit_all_call(const double* geo, const int* kinds, const int* code, int nobj,
+                                              const double* g, const Ray& r, double& t, int& face, double cut_m,
+                                              double cut_lim, bool cut_strict) {
+  return csg_hit_all(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
+}
+__device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, const int* code, int nobj,
+                                        const double* g, const Ray& r, double& t, int& face, double cut_m = 1.0,
+                                        double cut_lim = __builtin_inf(), bool cut_strict = true) {
+  constexpr int K = RT_CSG_LIVE > 0 ? RT_CSG_LIVE : 1;
+  if constexpr (RT_CSG_LIVE == 0) return csg_hit_all(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
+  const int* ci = reinterpret_cast<const int*>(g + 14);
+  const int first = nobj + ci[0], count = ci[1];
+  const int* prog = code + ci[2];
+  const int plen = ci[3];
+  const F3 of = f3(r.o), df = f3(r.d);
+  const float slack = ray_slack(of);
+  double LA[K], LB[K];
+  int LF[K];  // leaf index | entry face << 8 | exit face << 12
+#pragma unroll
+  for (int s = 0; s < K; s++) {
+    LA[s] = LB[s] = 0.0;
+    LF[s] = 0;
+  }
+  int n = 0;
+  for (int j = 0; j < count; j++) {
+    const int k = kinds[first + j];
+    const double* lg = geo + (size_t)(first + j) * GEO;
+    if (k != RT_PLANE && !may_hit(of, df, 3.0e38f, lg, slack)) continue;
+    double a, b;
+    int f;
+    leaf_interval(k, lg, r, a, b, f);
+    if (f & 256) {
+#pragma unroll
+      for (int s = 0; s < K; s++)
+        if (s == n) {
+          LA[s] = a;
+          LB[s] = b;
+          LF[s] = j | ((f & 0xff) << 8);
+        }
+      n++;
+    }
+  }
+  if (n > K) return csg_hit_all_call(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
+  double tc = 0.0;
+  for (;;) {
+    double te = __builtin_inf();
+    int se = -1, jend = 0;
+#pragma unroll
+    for (int s = 0; s < K; s++) {
+      if (s < n) {
+        if (LA[s] > tc && LA[s] < te) {
+          te = LA[s];
+          se = s;
+          jend = 0;
+        }
+        if (LB[s] > tc && LB[s] < te) {
+          te = LB[s];
+          se = s;
+          jend = 1;
+        }
+      }
+    }
+    if (se < 0) return false;
+    if (cut_strict ? te * cut_m > cut_lim : te * cut_m >= cut_lim) return false;
+    uint64_t b0 = 0, b1 = 0, a0 = 0, a1 = 0;
+    int fe = 0;
+#pragma unroll
+    for (int s = 0; s < K; s++) {
+      if (s < n) {
+        const int j = LF[s] & 0xff;
+        const uint64_t bit = 1ull << (j & 63);
+        const uint64_t bb = (LA[s] < te && te <= LB[s]) ? bit : 0ull;
+        const uint64_t ab = (LA[s] <= te && te < LB[s]) ? bit : 0ull;
+        if (j < 64) {
+          b0 |= bb;
+          a0 |= ab;
+        } else {
+          b1 |= bb;
+          a1 |= ab;
+        }
+      }
+      if (s == se) fe = LF[s];
+    }
+    const bool before = csg_eval(prog, plen, b0, b1), after = csg_eval(prog, plen, a0, a1);
+    if (before != after) {
+      const int flip = ((jend == 0) != after) ? 1 : 0;
+      t = te;
+      face = ((fe & 0xff) << 4) | (flip << 3) | (jend ? (fe >> 12) & 15 : (fe >> 8) & 15);
       return true;
     }
     tc = te;
@@ -1280,6 +1382,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   };
 
   PH_BEGIN();
+#ifdef RT_PHASE_TIMING
+  const uint64_t life_t0 = ph_t0_;
+#endif
   for (;;) {
     // ---- refill idle lanes from the wave pool (one 8x8 tile per chunk) ----
     for (;;) {
@@ -2152,6 +2257,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     atomicAdd(P.stats + ST_BVHDIAG + 3, (unsigned long long)bd_sleaf);
     atomicAdd(P.stats + ST_BVHDIAG + 4, (unsigned long long)bd_trays);
     atomicAdd(P.stats + ST_BVHDIAG + 5, (unsigned long long)bd_srays);
+    // wave lifetimes (main loop): mean vs max shows the load imbalance
+    const uint64_t life = stamp() - life_t0;
+    atomicAdd(P.stats + ST_BVHDIAG + 6, (unsigned long long)life);
+    atomicMax(P.stats + ST_BVHDIAG + 7, (unsigned long long)life);
 #endif
   }
   // Workgroup reduction of the per-lane counters (every wave of the group
