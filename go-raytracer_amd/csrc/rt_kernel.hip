@@ -39,7 +39,9 @@
 #include <chrono>
 #include <functional>
 #include <cmath>
+#include <array>
 #include <cstdio>
+#include <utility>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -65,14 +67,20 @@ __global__ void rt_debug_vm_kernel(const char* __restrict__ blob, int off_code, 
   err[i] = run_vm(code, consts, entry[prog], face[i], u[i], v[i], out + (size_t)i * 10) ? 1 : 0;
 }
 
-template __global__ void rt_render_kernel<true, false, false>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<false, false, false>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<true, true, false>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<false, true, false>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<true, false, true>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<false, false, true>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<true, true, true>(const char* __restrict__, Params);
-template __global__ void rt_render_kernel<false, true, true>(const char* __restrict__, Params);
+// The ahead-of-time flavours: <scene in LDS, BVH, CSG, pixel quads>, indexed
+// by kernel_index(); launch() picks one per scene.
+constexpr int kernel_index(bool lds, bool bvh, bool csg, bool quads) {
+  return (lds ? 1 : 0) | (bvh ? 2 : 0) | (csg ? 4 : 0) | (quads ? 8 : 0);
+}
+template <int I>
+constexpr const void* kernel_at() {
+  return (const void*)rt_render_kernel<(I & 1) != 0, (I & 2) != 0, (I & 4) != 0, (I & 8) != 0>;
+}
+template <int... I>
+constexpr std::array<const void*, sizeof...(I)> kernel_table(std::integer_sequence<int, I...>) {
+  return {kernel_at<I>()...};
+}
+const std::array<const void*, 16> k_kernels = kernel_table(std::make_integer_sequence<int, 16>{});
 // ===========================================================================
 // Host side: scene conversion (raytracer.go:724-830) and the C ABI
 // ===========================================================================
@@ -570,10 +578,11 @@ struct SpecKey {
   int kmask = 0, feat = 0, nlights = 0;  // nlights > 0: light loop unrolled for that count
   int pow_bits = 7;                      // unrolled specular powering steps
   int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
+  int quads = 0;                         // pixel quads (use_quads)
   std::string str() const {
     return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
            std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits) +
-           ":" + std::to_string(nocull);
+           ":" + std::to_string(nocull) + ":" + std::to_string(quads);
   }
 };
 
@@ -651,6 +660,17 @@ void csg_mask_program(const int* code, int len, std::vector<int>& out) {
 // Scene blob staged in LDS (small scenes) or read from global memory with
 // wave-uniform scalar loads. RT_SCENE_GLOBAL=1 forces the global flavour
 // (tuning experiments only).
+// Pixel quads (rt_render.h QUADS): a pixel's 4 samples in 4 lanes at once.
+// They pay where per-pixel work is long and uneven -- recursion depth >= 7
+// (C4, C5, canned, c4csg: the glass trees of the last pixels otherwise keep a
+// few waves running long after the rest); at shallower depths the idle
+// siblings cost more than the balance gains (C2, C3). RT_PIXEL_QUADS=0/1
+// forces the choice (tests, experiments).
+bool use_quads(const DevScene& s) {
+  if (const char* e = getenv("RT_PIXEL_QUADS")) return atoi(e) != 0;
+  return s.depth >= 7;
+}
+
 bool scene_in_lds(const DevScene& s) {
   static const bool force_global = getenv("RT_SCENE_GLOBAL") && atoi(getenv("RT_SCENE_GLOBAL")) != 0;
   return !force_global && s.blob_bytes <= (int)LDS_MAX_BYTES;
@@ -671,6 +691,7 @@ bool spec_key(const DevScene& s, SpecKey* k) {
             ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
   k->nlights = (s.nlights >= 1 && s.nlights <= SPEC_MAX_LIGHTS) ? s.nlights : 0;
   k->pow_bits = s.num_programs ? 7 : s.pow_bits;  // surface programs set exponents at run time
+  k->quads = use_quads(s) ? 1 : 0;
   return true;
 }
 
@@ -709,7 +730,8 @@ int spec_compile(const SpecKey& sk, double* ms) {
   }
   for (const auto& x : extra) opts.push_back(x.c_str());
   const std::string name = std::string("rt_render_kernel<") + (sk.lds ? "true" : "false") + ", " +
-                           (sk.bvh ? "true" : "false") + ", " + (sk.csg ? "true" : "false") + ">";
+                           (sk.bvh ? "true" : "false") + ", " + (sk.csg ? "true" : "false") + ", " +
+                           (sk.quads ? "true" : "false") + ">";
   const char* name_expr = name.c_str();
   hiprtcProgram prog;
   hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
@@ -862,12 +884,12 @@ int rt_create(int device, rt_context** out) {
   // Persistent grids: as many workgroups as are resident (any extra block just
   // finds the queue drained). The LDS flavour is sized for the LDS budget.
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true, false, false>, WG, LDS_MAX_BYTES) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_kernels[kernel_index(true, false, false, false)], WG, LDS_MAX_BYTES) !=
           hipSuccess || per_cu <= 0)
     per_cu = 2;
   c->grid_lds = c->cus * std::min(per_cu, 8);
   per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false, false, false>, WG, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_kernels[kernel_index(false, false, false, false)], WG, 0) != hipSuccess ||
       per_cu <= 0)
     per_cu = 2;
   c->grid_glb = c->cus * std::min(per_cu, 8);
@@ -891,7 +913,7 @@ int rt_create(int device, rt_context** out) {
     }
   }
   int rc = upload(&c->jump, jump);
-  if (rc == RT_OK && hipMalloc((void**)&c->queue, 256) != hipSuccess) rc = fail(RT_E_NOMEM, "queue alloc");
+  if (rc == RT_OK && hipMalloc((void**)&c->queue, 512) != hipSuccess) rc = fail(RT_E_NOMEM, "queue alloc");
   if (rc == RT_OK && hipMalloc((void**)&c->stats, sizeof(unsigned long long) * 64) != hipSuccess)
     rc = fail(RT_E_NOMEM, "stats alloc");
   if (rc == RT_OK && hipMemset(c->stats, 0, sizeof(unsigned long long) * 64) != hipSuccess)
@@ -1381,13 +1403,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
-  const void* kfn;
-  if (s.has_csg)
-    kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, true> : (const void*)rt_render_kernel<true, false, true>)
-              : (s.use_bvh ? (const void*)rt_render_kernel<false, true, true> : (const void*)rt_render_kernel<false, false, true>);
-  else
-    kfn = lds ? (s.use_bvh ? (const void*)rt_render_kernel<true, true, false> : (const void*)rt_render_kernel<true, false, false>)
-              : (s.use_bvh ? (const void*)rt_render_kernel<false, true, false> : (const void*)rt_render_kernel<false, false, false>);
+  const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, use_quads(s))];
   hipFunction_t spec = c->spec_fn;  // built for this scene's flavour (spec_key)
   auto occupancy = [&](int bytes) {
     int n = 0;
@@ -1485,25 +1501,14 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     P.bvh_stack_off = stack_off;
   }
 
-  HIP_TRY(hipMemsetAsync(c->queue, 0, 256, st));
+  HIP_TRY(hipMemsetAsync(c->queue, 0, 512, st));  // QHEADS queue heads, 64 B apart
   HIP_TRY(hipEventRecord(c->ev0, st));
   const char* blob = s.blob;
-#define RT_LAUNCH(L, B, Cs) hipLaunchKernelGGL((rt_render_kernel<L, B, Cs>), dim3(grid), dim3(WG), shmem, st, blob, P)
-  if (spec) {
-    void* args[] = {(void*)&blob, (void*)&P};
+  void* args[] = {(void*)&blob, (void*)&P};
+  if (spec)
     HIP_TRY(hipModuleLaunchKernel(spec, grid, 1, 1, WG, 1, 1, shmem, st, args, nullptr));
-  } else if (s.has_csg) {
-    if (lds && s.use_bvh) RT_LAUNCH(true, true, true);
-    else if (lds) RT_LAUNCH(true, false, true);
-    else if (s.use_bvh) RT_LAUNCH(false, true, true);
-    else RT_LAUNCH(false, false, true);
-  } else {
-    if (lds && s.use_bvh) RT_LAUNCH(true, true, false);
-    else if (lds) RT_LAUNCH(true, false, false);
-    else if (s.use_bvh) RT_LAUNCH(false, true, false);
-    else RT_LAUNCH(false, false, false);
-  }
-#undef RT_LAUNCH
+  else
+    HIP_TRY(hipLaunchKernel(kfn, dim3(grid), dim3(WG), args, shmem, st));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   c->timed = true;

@@ -118,10 +118,16 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
 // material is both reflective and transparent) always live in HBM.
 enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
+// Work queue: pixels per dequeue -- one 8x8 tile, or with pixel quads a 4x4
+// quarter of one (16 quads = one wave's lanes) -- from QHEADS queue heads
+// (chunk c belongs to head c mod QHEADS; a workgroup starts on head blockIdx
+// mod QHEADS and moves to the others once it is drained), so the dequeue rate
+// stays below what one atomic word sustains.
+enum { QHEADS = 8, QSTRIDE = 16 /* u32 between heads: 64 B */ };
 enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
        ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32 };  // (stats buffer: 64 entries)
-enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2 };
+enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };  // S_DONE: sample colour held for the quad
 #ifndef RT_LDS_MAX
 #define RT_LDS_MAX (40 * 1024)
 #endif
@@ -1128,12 +1134,22 @@ struct View {
   const int* csg;        // CSG postfix programs (extension)
 };
 
-template <bool LDS, bool BVH, bool CSG>
+// QUADS (pixel quads): a pixel's 4 samples run at once in 4 adjacent lanes,
+// not one after another in one lane -- 4x shorter per-pixel latency, so the
+// deep, branching trees of glass at depth >= 7 no longer leave a few waves
+// running long after the rest (host choice per scene, rt_kernel.hip).
+template <bool LDS, bool BVH, bool CSG, bool QUADS>
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 3  // 168 VGPRs -> 3 waves/SIMD (C3 on par with 4; C2 -10%, C4 (BVH) -4%)
 #endif
 __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char* __restrict__ blob, Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef RT_COST_MAP
+  constexpr bool QD = false;  // the cost-map diagnostic charges all of a pixel's work to one lane
+#else
+  constexpr bool QD = QUADS;
+#endif
+  constexpr unsigned int QCHUNK = QD ? 16u : 64u;
   const char* base;
   // Stage the PCG jump table (and, LDS flavour, the whole scene) once per
   // workgroup (the only block-wide barrier).
@@ -1272,6 +1288,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 
   // wave-uniform pool and counters
   unsigned int pool_next = 0, pool_end = 0;
+  int qhead = 0;  // queue heads tried so far (QHEADS)
   bool exhausted = false;
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off);
   for (int k = 0; k < NCNT; k++) cnt[k * WG + threadIdx.x] = 0;
@@ -1307,6 +1324,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     while (__any(have_res)) {
       if (have_res) {
         if (sp == 0) {
+          if constexpr (QD) {
+            sum = res;  // this sample's colour, summed by the quad's first lane (main loop)
+            state = S_DONE;
+          } else {
           sum = add(sum, res);  // raytracer.go:651
           sample++;
           if (sample == 4) {
@@ -1325,6 +1346,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           } else {
             need_gen = true;  // next sample ray, generated in one uniform block
             state = S_TRACE;
+          }
           }
           have_res = false;
         } else {
@@ -1386,32 +1408,71 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   const uint64_t life_t0 = ph_t0_;
 #endif
   for (;;) {
+    // ---- quads whose 4 samples are all done: the first lane adds the
+    // colours in sample order (raytracer.go:651) and quantises
+    // (raytracer.go:656, vec.go:104-107); the quad becomes idle ----
+    if constexpr (QD) {
+      const uint64_t dn = __ballot(state == S_DONE);
+      const uint64_t qd = dn & (dn >> 1) & (dn >> 2) & (dn >> 3) & 0x1111111111111111ull;
+      if (qd) {
+        // running sum (((0 + s0) + s1) + s2) + s3, one neighbour's colour at a time
+        d3 sm = add(mk(0, 0, 0), sum);
+#pragma unroll
+        for (int k = 1; k < 4; k++) {
+          const int lk = (lane + k) & 63;
+          sm = add(sm, mk(__shfl(sum.x, lk), __shfl(sum.y, lk), __shfl(sum.z, lk)));
+        }
+        if ((qd >> lane) & 1) {
+          const d3 c = scale(sm, 1.0 / 4.0);
+          const uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
+          const uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
+          const uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
+          P.out[pout] = (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+        }
+        if ((qd >> (lane & ~3)) & 1) state = S_IDLE;
+      }
+    }
     // ---- refill idle lanes from the wave pool (one 8x8 tile per chunk) ----
     for (;;) {
-      bool need = state == S_IDLE;
-      uint64_t mask = __ballot(need);
+      // with quads a pixel goes to a quad whose 4 lanes are all idle, sample k
+      // to lane 4p+k; mask = the idle lanes / the idle quads' first lanes
+      const uint64_t il = __ballot(state == S_IDLE);
+      const uint64_t mask = QD ? il & (il >> 1) & (il >> 2) & (il >> 3) & 0x1111111111111111ull : il;
+      const bool need = ((mask >> (QD ? (lane & ~3) : lane)) & 1) != 0;
       if (mask == 0 || exhausted) break;
       if (pool_next >= pool_end) {
-        unsigned int b = 0;
-        if (lane == 0) b = atomicAdd(P.queue, (unsigned int)CHUNK);
-        b = __shfl(b, 0);
-        if (b >= P.total_slots) {
+        const unsigned int nchunks = (P.total_slots + QCHUNK - 1) / QCHUNK;
+        unsigned int c = nchunks;
+        while (qhead < QHEADS) {
+          const unsigned int h = (blockIdx.x + qhead) % QHEADS;
+          unsigned int n = 0;
+          if (lane == 0) n = atomicAdd(P.queue + h * QSTRIDE, 1u);
+          c = __builtin_amdgcn_readfirstlane(n) * QHEADS + h;
+          if (c < nchunks) break;
+          qhead++;  // this head is drained: try the next one
+        }
+        if (qhead >= QHEADS) {
           exhausted = true;
           break;
         }
-        pool_next = b;
-        pool_end = min(b + (unsigned int)CHUNK, P.total_slots);
+        pool_next = c * QCHUNK;
+        pool_end = min(pool_next + (unsigned int)QCHUNK, P.total_slots);
       }
-      unsigned int rank = __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
+      // idle lanes (quads) before mine
+      const unsigned int rank = QD ? (unsigned int)__popcll(mask & ((1ull << (lane & ~3)) - 1ull))
+                                   : __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
       unsigned int take = min((unsigned int)__popcll(mask), pool_end - pool_next);
       if (need && rank < take) {
         unsigned int slot = pool_next + rank;
         unsigned int tile = slot / (TILE * TILE), within = slot % (TILE * TILE);
+        // quads: a 16-pixel chunk is a 4x4 quarter of the tile
+        const int tx = QD ? (int)(((within >> 4) & 1u) * 4u + (within & 3u)) : (int)(within % TILE);
+        const int ty = QD ? (int)((within >> 5) * 4u + ((within >> 2) & 3u)) : (int)(within / TILE);
         const int trow = (int)(tile / (unsigned)P.tiles_x);
-        const int x = (int)((tile % (unsigned)P.tiles_x) * TILE + within % TILE);
-        const int orow = trow * TILE + (int)(within / TILE);
-        const int y = P.trow_stride > 0 ? (P.trow0 + trow * P.trow_stride) * TILE + (int)(within / TILE) : P.y0 + orow;
+        const int x = (int)((tile % (unsigned)P.tiles_x) * TILE + tx);
+        const int orow = trow * TILE + ty;
+        const int y = P.trow_stride > 0 ? (P.trow0 + trow * P.trow_stride) * TILE + ty : P.y0 + orow;
         if (x < P.width && y < P.y1) {
           px = x;
           py = y;
@@ -1422,7 +1483,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
           const uint64_t* j = jtab + (y % 20) * 4;
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
-          sample = 0;
+          sample = QD ? (lane & 3) : 0;
+          if constexpr (QD) rng = pcg_skip_samples(rng, sample);
           sum = mk(0, 0, 0);
           sp = 0;
           need_gen = true;

@@ -655,3 +655,38 @@ def test_fractional_specular_and_spot_exponents_match_oracle(ctx, spec_ctx):
         img, st = render(c, packed)
         assert_same(img, ref, "fractional exponents")
         assert st.as_dict() == ost.as_dict()
+
+
+# --- work distribution: pixel quads (a pixel's 4 samples in 4 lanes at once,
+# chosen for depth >= 7) and one sample after another in one lane must give
+# the same bytes and counters, in both kernels.
+
+@pytest.mark.parametrize("case", ["c3", "c4", "canned", "mixed", "csg"])
+def test_pixel_quads_and_serial_samples_match_oracle(ctx, spec_ctx, case):
+    if case == "c3":
+        args = rt.configs.c3(width=112, height=72)
+    elif case == "c4":
+        args = rt.configs.c4(width=96, height=64)
+    elif case == "canned":
+        args = rt.configs.canned(width=100, height=60)
+    elif case == "mixed":
+        args = _mixed_scene(9, 40, 72, 52, depth=8)
+    else:
+        args = _csg_scene(3, 6, 80, 56)
+        args = replace(args, depth=8)
+    packed = rt.scene.convert(args)
+    ref, ost = oracle_bind.render_rows(packed)
+    old = os.environ.get("RT_PIXEL_QUADS")
+    try:
+        for quads in ("0", "1"):
+            os.environ["RT_PIXEL_QUADS"] = quads
+            for c in (ctx, spec_ctx):
+                c.set_scene(packed)  # the choice is made per scene
+                img, st = render(c, packed)
+                assert_same(img, ref, "%s quads=%s" % (case, quads))
+                assert st.as_dict() == ost.as_dict()
+    finally:
+        if old is None:
+            os.environ.pop("RT_PIXEL_QUADS", None)
+        else:
+            os.environ["RT_PIXEL_QUADS"] = old
