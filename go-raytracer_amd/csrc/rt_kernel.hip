@@ -437,6 +437,7 @@ int align16(int v) { return (v + 15) & ~15; }
 struct rt_context {
   int device = 0;
   int last_waves = 0, launches = 0;  // diagnostics (RT_PHASE_TIMING wave lifetimes)
+  int sched = RT_SCHED_AUTO;         // rt_set_schedule
   int cus = 0;
   int lds_per_cu = 0, lds_per_block = 0;  // bytes (device properties)
   int grid_lds = 0, grid_glb = 0;  // persistent grids (workgroups) per kernel flavour
@@ -664,10 +665,14 @@ void csg_mask_program(const int* code, int len, std::vector<int>& out) {
 // They pay where per-pixel work is long and uneven -- recursion depth >= 7
 // (C4, C5, canned, c4csg: the glass trees of the last pixels otherwise keep a
 // few waves running long after the rest); at shallower depths the idle
-// siblings cost more than the balance gains (C2, C3). RT_PIXEL_QUADS=0/1
-// forces the choice (tests, experiments).
-bool use_quads(const DevScene& s) {
-  if (const char* e = getenv("RT_PIXEL_QUADS")) return atoi(e) != 0;
+// siblings cost more than the balance gains (C2, C3). rt_set_schedule
+// overrides the choice; so does RT_PIXEL_QUADS=0/1 in the environment at
+// process start (experiments).
+bool use_quads(int sched, const DevScene& s) {
+  static const int env = getenv("RT_PIXEL_QUADS") ? atoi(getenv("RT_PIXEL_QUADS")) : -1;
+  if (env >= 0) return env != 0;
+  if (sched == RT_SCHED_PIXEL) return false;
+  if (sched == RT_SCHED_QUADS) return true;
   return s.depth >= 7;
 }
 
@@ -691,7 +696,6 @@ bool spec_key(const DevScene& s, SpecKey* k) {
             ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
   k->nlights = (s.nlights >= 1 && s.nlights <= SPEC_MAX_LIGHTS) ? s.nlights : 0;
   k->pow_bits = s.num_programs ? 7 : s.pow_bits;  // surface programs set exponents at run time
-  k->quads = use_quads(s) ? 1 : 0;
   return true;
 }
 
@@ -798,6 +802,7 @@ int spec_prepare(rt_context* c) {
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
+  sk.quads = use_quads(c->sched, c->sc) ? 1 : 0;
   std::lock_guard<std::mutex> lock(g_spec_mu);
   return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
 }
@@ -813,6 +818,14 @@ int rt_set_accel(rt_context* c, int flags) {
   if (flags & ~(RT_ACCEL_BVH | RT_ACCEL_CULL)) return fail(RT_E_INVALID, "rt_set_accel: unknown flags");
   c->accel = flags;
   return spec_prepare(c);
+}
+
+int rt_set_schedule(rt_context* c, int mode) {
+  if (!c) return fail(RT_E_INVALID, "rt_set_schedule: NULL context");
+  if (mode != RT_SCHED_AUTO && mode != RT_SCHED_PIXEL && mode != RT_SCHED_QUADS)
+    return fail(RT_E_INVALID, "rt_set_schedule: unknown mode");
+  c->sched = mode;
+  return RT_OK;
 }
 
 int rt_set_specialize(rt_context* c, int enable) {
@@ -1403,7 +1416,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
-  const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, use_quads(s))];
+  const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, use_quads(c->sched, s))];
   hipFunction_t spec = c->spec_fn;  // built for this scene's flavour (spec_key)
   auto occupancy = [&](int bytes) {
     int n = 0;

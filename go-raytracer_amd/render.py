@@ -63,6 +63,8 @@ def load_library(path=None):
     l.rt_set_specialize.restype = i
     l.rt_set_accel.argtypes = [vp, i]
     l.rt_set_accel.restype = i
+    l.rt_set_schedule.argtypes = [vp, i]
+    l.rt_set_schedule.restype = i
     l.rt_scene_info.argtypes = [vp, C.POINTER(i)]
     l.rt_scene_info.restype = i
     l.rt_specialized.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
@@ -135,6 +137,12 @@ class RenderContext:
         identical pixels and counters). The BVH choice applies at the next
         set_scene; culling applies to specialised kernels."""
         _check(self.lib.rt_set_accel(self.handle, int(flags)), "rt_set_accel")
+
+    def set_schedule(self, mode):
+        """abi.RT_SCHED_AUTO (default: pixel quads for depth >= 7),
+        RT_SCHED_PIXEL or RT_SCHED_QUADS -- how pixels are dealt to lanes;
+        identical pixels and counters. Applies at the next set_scene."""
+        _check(self.lib.rt_set_schedule(self.handle, int(mode)), "rt_set_schedule")
 
     def scene_info(self):
         """rt_scene_info flags of the current scene (abi.RT_INFO_*): which

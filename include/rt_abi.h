@@ -318,14 +318,26 @@ int rt_set_specialize(rt_context *ctx, int enable);
 #define RT_ACCEL_CULL 2
 int rt_set_accel(rt_context *ctx, int flags);
 
+/* How pixels are dealt to the device lanes (MI355X-specific; pixels and
+ * counters are identical in every mode). RT_SCHED_PIXEL: a lane renders a
+ * pixel's 4 samples one after another (raytracer.go:645-651), 64 pixels per
+ * dequeue. RT_SCHED_QUADS: a pixel's 4 samples run at once in 4 adjacent
+ * lanes whose first lane adds them in sample order, 16 pixels per dequeue --
+ * 4x shorter per-pixel latency, so deep branching glass trees do not leave a
+ * few waves running long after the rest. RT_SCHED_AUTO (default): quads for
+ * depth >= 7. Takes effect at the next rt_set_scene. */
+#define RT_SCHED_AUTO 0
+#define RT_SCHED_PIXEL 1
+#define RT_SCHED_QUADS 2
+int rt_set_schedule(rt_context *ctx, int mode);
+
 /* How the current scene is laid out for the device (bit flags), e.g. for
  * tests that must exercise one kernel flavour: RT_INFO_LDS the scene blob is
  * staged in LDS per workgroup; RT_INFO_BVH a BVH over the bounded objects;
  * RT_INFO_CSG CSG composites; RT_INFO_STREAM a large linear scene whose
- * object records stream through per-wave LDS chunks in the megakernel;
- * RT_INFO_WAVEFRONT a large linear scene rendered by the level-synchronous
- * wavefront path (separate trace / shade kernels, rt_set_accel without
- * RT_ACCEL_BVH). */
+ * object records are read from global memory in index order (per-wave LDS
+ * chunks, or scalar loads in the brute-force kernel); RT_INFO_WAVEFRONT is
+ * reserved (never set). */
 #define RT_INFO_LDS 1
 #define RT_INFO_BVH 2
 #define RT_INFO_CSG 4

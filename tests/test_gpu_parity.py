@@ -676,17 +676,13 @@ def test_pixel_quads_and_serial_samples_match_oracle(ctx, spec_ctx, case):
         args = replace(args, depth=8)
     packed = rt.scene.convert(args)
     ref, ost = oracle_bind.render_rows(packed)
-    old = os.environ.get("RT_PIXEL_QUADS")
     try:
-        for quads in ("0", "1"):
-            os.environ["RT_PIXEL_QUADS"] = quads
+        for mode in (rt.abi.RT_SCHED_PIXEL, rt.abi.RT_SCHED_QUADS):
             for c in (ctx, spec_ctx):
-                c.set_scene(packed)  # the choice is made per scene
-                img, st = render(c, packed)
-                assert_same(img, ref, "%s quads=%s" % (case, quads))
+                c.set_schedule(mode)
+                img, st = render(c, packed)  # the schedule applies at set_scene
+                assert_same(img, ref, "%s schedule %d" % (case, mode))
                 assert st.as_dict() == ost.as_dict()
     finally:
-        if old is None:
-            os.environ.pop("RT_PIXEL_QUADS", None)
-        else:
-            os.environ["RT_PIXEL_QUADS"] = old
+        for c in (ctx, spec_ctx):
+            c.set_schedule(rt.abi.RT_SCHED_AUTO)
