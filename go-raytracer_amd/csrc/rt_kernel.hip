@@ -247,6 +247,7 @@ struct DevScene {
   bool use_bvh = false;
   int nplanes = 0, nnodes = 0, kind_mask = 0;
   int light_mask = 0;  // bit k: the scene has lights of kind k (RT_LIGHT_*)
+  bool branching = false;  // some material is reflective and transparent (or a surface program decides)
   int leaf_kind_mask = 0;  // bit k: some CSG leaf has kind k
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0;
   int nruns = 0;
@@ -434,10 +435,35 @@ int align16(int v) { return (v + 15) & ~15; }
 
 }  // namespace
 
+// What a specialised kernel is compiled for. Serialised as the cache key
+// "lds:bvh:csg:nobj:kinds:kmask:feat"; nobj > 0 (kinds = "k0,k1,...") unrolls the
+// object loops of a small linear LDS scene, nobj = 0 only fixes the kind mask
+// and the feature bits (BVH, global-memory and larger linear scenes).
+struct SpecKey {
+  int lds = 1, bvh = 0, csg = 0, nobj = 0;
+  std::string kinds;
+  int kmask = 0, feat = 0, nlights = 0;  // nlights > 0: light loop unrolled for that count
+  int pow_bits = 7;                      // unrolled specular powering steps
+  int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
+  int quads = 0;                         // pixel quads (use_quads)
+  std::string str() const {
+    return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
+           std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits) +
+           ":" + std::to_string(nocull) + ":" + std::to_string(quads);
+  }
+};
+
+// Launch configuration of one (kernel, fixed LDS, frames) combination.
+struct LaunchPlan {
+  const void* fn = nullptr;
+  int shmem_fixed = -1, frames = 0, per_cu = 0, lds_levels = 0, lds_full = 0;
+};
+
 struct rt_context {
   int device = 0;
   int last_waves = 0, launches = 0;  // diagnostics (RT_PHASE_TIMING wave lifetimes)
   int sched = RT_SCHED_AUTO;         // rt_set_schedule
+  LaunchPlan plan;                   // last launch's occupancy / LDS plan
   int cus = 0;
   int lds_per_cu = 0, lds_per_block = 0;  // bytes (device properties)
   int grid_lds = 0, grid_glb = 0;  // persistent grids (workgroups) per kernel flavour
@@ -460,6 +486,8 @@ struct rt_context {
   bool specialize = false;
   int accel = RT_ACCEL_BVH | RT_ACCEL_CULL;  // rt_set_accel
   hipFunction_t spec_fn = nullptr;  // specialised kernel of the current scene, if any
+  hipFunction_t spec_alt_fn = nullptr;  // ... for the other pixel schedule (spec_for)
+  SpecKey spec_key;                     // what spec_fn was compiled for
   double spec_ms = 0;               // hipRTC compile time of spec_fn (0 = cache hit)
 };
 
@@ -569,23 +597,6 @@ bool rtc_load() {
   return true;
 }
 
-// What a specialised kernel is compiled for. Serialised as the cache key
-// "lds:bvh:csg:nobj:kinds:kmask:feat"; nobj > 0 (kinds = "k0,k1,...") unrolls the
-// object loops of a small linear LDS scene, nobj = 0 only fixes the kind mask
-// and the feature bits (BVH, global-memory and larger linear scenes).
-struct SpecKey {
-  int lds = 1, bvh = 0, csg = 0, nobj = 0;
-  std::string kinds;
-  int kmask = 0, feat = 0, nlights = 0;  // nlights > 0: light loop unrolled for that count
-  int pow_bits = 7;                      // unrolled specular powering steps
-  int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
-  int quads = 0;                         // pixel quads (use_quads)
-  std::string str() const {
-    return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
-           std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits) +
-           ":" + std::to_string(nocull) + ":" + std::to_string(quads);
-  }
-};
 
 // CSG membership program for the device (csg_eval): the composite's postfix
 // program (include/rt_abi.h RT_CSG) with every maximal union-only or
@@ -662,18 +673,25 @@ void csg_mask_program(const int* code, int len, std::vector<int>& out) {
 // wave-uniform scalar loads. RT_SCENE_GLOBAL=1 forces the global flavour
 // (tuning experiments only).
 // Pixel quads (rt_render.h QUADS): a pixel's 4 samples in 4 lanes at once.
-// They pay where per-pixel work is long and uneven -- recursion depth >= 7
-// (C4, C5, canned, c4csg: the glass trees of the last pixels otherwise keep a
-// few waves running long after the rest); at shallower depths the idle
-// siblings cost more than the balance gains (C2, C3). rt_set_schedule
-// overrides the choice; so does RT_PIXEL_QUADS=0/1 in the environment at
-// process start (experiments).
-bool use_quads(int sched, const DevScene& s) {
+// They pay where the longest pixels, not the total work, set the frame time:
+// recursion depth >= 7 (C4, C5, canned, c4csg: the glass trees of the last
+// pixels otherwise keep a few waves running long after the rest), and scenes
+// with branching materials (reflective and transparent: binary ray trees)
+// when a launch gives each lane fewer than 32 pixels -- a strong-scaling
+// share of a frame (C3 over 2 / 4 / 8 ranks: 2.37 / 1.78 / 1.40 ms serial vs
+// 2.11 / 1.07 / 0.64 ms with quads) -- and any scene below 4 pixels per lane
+// (C2 over 4 / 8 ranks: 0.22 / 0.19 vs 0.18 / 0.14 ms). Otherwise the idle
+// siblings cost more than the balance gains (C3 whole frame 3.67 vs 4.30 ms,
+// C2 0.38 vs 0.45 ms).
+// rt_set_schedule overrides the choice; so does RT_PIXEL_QUADS=0/1 in the
+// environment at process start (experiments).
+bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus) {
   static const int env = getenv("RT_PIXEL_QUADS") ? atoi(getenv("RT_PIXEL_QUADS")) : -1;
   if (env >= 0) return env != 0;
   if (sched == RT_SCHED_PIXEL) return false;
   if (sched == RT_SCHED_QUADS) return true;
-  return s.depth >= 7;
+  const double lanes = (double)std::max(1, cus) * 4 * 3 * 64;  // 3 waves per SIMD
+  return s.depth >= 7 || (double)pixels < (s.branching ? 32.0 : 4.0) * lanes;
 }
 
 bool scene_in_lds(const DevScene& s) {
@@ -802,9 +820,30 @@ int spec_prepare(rt_context* c) {
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
-  sk.quads = use_quads(c->sched, c->sc) ? 1 : 0;
+  sk.quads = use_quads(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus) ? 1 : 0;
+  c->spec_key = sk;
+  c->spec_alt_fn = nullptr;
   std::lock_guard<std::mutex> lock(g_spec_mu);
   return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
+}
+
+// The specialised kernel for `quads` (the scene's other schedule is compiled
+// on first use: a launch covering a small share of the frame).
+int spec_for(rt_context* c, bool quads, hipFunction_t* fn) {
+  if (!c->spec_fn || (c->spec_key.quads != 0) == quads) {
+    *fn = c->spec_fn;
+    return RT_OK;
+  }
+  if (!c->spec_alt_fn) {
+    SpecKey sk = c->spec_key;
+    sk.quads = quads ? 1 : 0;
+    double ms = 0;
+    std::lock_guard<std::mutex> lock(g_spec_mu);
+    int rc = spec_build(c->device, sk, &c->spec_alt_fn, &ms);
+    if (rc != RT_OK) return rc;
+  }
+  *fn = c->spec_alt_fn;
+  return RT_OK;
 }
 
 }  // namespace
@@ -1168,6 +1207,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   std::vector<double> mats((size_t)s.nmats * MAT, 0.0);
   for (int m = 0; m < s.nmats; m++) {
     const rt_material& mm = in->materials[m];
+    if (mm.reflectivity > 0 && mm.transparency > 0) s.branching = true;
     double* d = &mats[(size_t)m * MAT];
     d[0] = mm.color[0];
     d[1] = mm.color[1];
@@ -1416,8 +1456,14 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
-  const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, use_quads(c->sched, s))];
-  hipFunction_t spec = c->spec_fn;  // built for this scene's flavour (spec_key)
+  const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
+  const bool quads = use_quads(c->sched, s, launch_pixels, c->cus);
+  const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
+  hipFunction_t spec = nullptr;  // built for this scene's flavour (spec_key), this schedule
+  {
+    int rc = spec_for(c, quads, &spec);
+    if (rc != RT_OK) return rc;
+  }
   auto occupancy = [&](int bytes) {
     int n = 0;
     if (spec) {
@@ -1427,7 +1473,13 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     }
     return n;
   };
-  int per_cu = occupancy(shmem);
+  // The occupancy queries take host time comparable to a small launch (a
+  // strong-scaling share of a frame), so the plan is kept per (kernel, LDS).
+  const void* plan_fn = spec ? (const void*)spec : kfn;
+  const int frames = std::max(1, s.depth - 1);
+  LaunchPlan& pl = c->plan;
+  const bool plan_hit = pl.fn == plan_fn && pl.shmem_fixed == shmem && pl.frames == frames;
+  int per_cu = plan_hit ? pl.per_cu : occupancy(shmem);
   if (per_cu <= 0) per_cu = 1;
   // The frame cores of the shallowest recursion levels live in the LDS that
   // is left over at this occupancy (never lowering it); deeper levels stay in
@@ -1436,9 +1488,8 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // child's colour, pending refraction ray) of the first n levels to LDS.
   const int level_bytes = WAVES_PER_WG * CORE * 64 * (int)sizeof(double);
   const int ext_bytes = WAVES_PER_WG * 9 * 64 * (int)sizeof(double);
-  const int frames = std::max(1, s.depth - 1);
-  int lds_levels = 0, lds_full = 0;
-  if (c->lds_per_cu > 0 && c->lds_per_block > 0) {
+  int lds_levels = plan_hit ? pl.lds_levels : 0, lds_full = plan_hit ? pl.lds_full : 0;
+  if (!plan_hit && c->lds_per_cu > 0 && c->lds_per_block > 0) {
     const int avail = std::min(c->lds_per_block, c->lds_per_cu / std::min(per_cu, 8)) - shmem;
     if (const char* e = getenv("RT_LDS_FULL")) lds_full = std::max(0, std::min(frames, atoi(e)));
     while (lds_full > 0 && lds_full * (ext_bytes + level_bytes) > avail) lds_full--;
@@ -1449,6 +1500,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
       lds_full = std::min(lds_full, lds_levels);
     }
   }
+  if (!plan_hit) pl = LaunchPlan{plan_fn, shmem, frames, per_cu, lds_levels, lds_full};
   const int ext_off = shmem + lds_levels * level_bytes;
   shmem = ext_off + lds_full * ext_bytes;
   static const bool dbg = getenv("RT_DEBUG_LAUNCH") != nullptr;

@@ -124,6 +124,9 @@ enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
 // mod QHEADS and moves to the others once it is drained), so the dequeue rate
 // stays below what one atomic word sustains.
 enum { QHEADS = 8, QSTRIDE = 16 /* u32 between heads: 64 B */ };
+#ifndef RT_QCHUNK_PIXEL
+#define RT_QCHUNK_PIXEL 64  // pixels per dequeue without quads (a multiple of 16 dividing 64)
+#endif
 enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
        ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32 };  // (stats buffer: 64 entries)
@@ -1149,7 +1152,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #else
   constexpr bool QD = QUADS;
 #endif
-  constexpr unsigned int QCHUNK = QD ? 16u : 64u;
+  constexpr unsigned int QCHUNK = QD ? 16u : (unsigned int)RT_QCHUNK_PIXEL;
   const char* base;
   // Stage the PCG jump table (and, LDS flavour, the whole scene) once per
   // workgroup (the only block-wide barrier).

@@ -1,0 +1,46 @@
+"""Strong-scaling rehearsal on ONE GPU: the kernel time of rank 0's share of a
+frame (interleaved 8-row tile rows, stride = world) for world = 1, 2, 4, 8, as
+bench.py --scaling strong would launch it on each rank (no collective here).
+efficiency(world) = t(1) / (world * t(world)).
+usage: python scripts/strong_emul.py [config] [steps]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from __graft_entry__ import load_package  # noqa: E402
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    pkg = load_package()
+    import torch
+    torch.cuda.set_device(0)
+    packed = pkg.scene.convert(pkg.configs.CONFIGS[cfg]())
+    ctx = pkg.RenderContext(0, specialize=True)
+    ctx.set_scene(packed)
+    out = {"config": cfg}
+    t1 = None
+    for world in (1, 2, 4, 8):
+        dr = pkg.dist.DistributedRenderer(ctx, packed, 0, world, torch.device("cuda", 0), mode="interleaved")
+        for _ in range(3):
+            dr.step(gather=False)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t0 = time.perf_counter()
+        for k in range(steps):
+            dr.step(gather=False, events=ev[k])
+        torch.cuda.synchronize()
+        out["w%d_wall_ms" % world] = round((time.perf_counter() - t0) / steps * 1e3, 4)
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        t1 = t1 or ms
+        out["w%d_ms" % world] = round(ms, 4)
+        out["w%d_eff" % world] = round(t1 / (world * ms), 3)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
