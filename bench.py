@@ -183,7 +183,9 @@ def main():
             raise SystemExit("--rows is a one-GPU measurement")
         band = tuple(int(v) for v in args.rows.split(":"))
         mode = "band"
-    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=mode, band=band)
+    # strong scaling over several ranks: frame k's gather overlaps frame k+1's render
+    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=mode, band=band,
+                                      pipeline=args.scaling == "strong")
 
     def barrier():
         if world > 1:
@@ -191,6 +193,7 @@ def main():
 
     for _ in range(args.warmup):
         dr.step()
+    dr.flush()
     torch.cuda.synchronize()
     ctx.read_stats(reset=True)
 
@@ -203,6 +206,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         dr.step(events=evs[k])
+    dr.flush()  # every frame gathered to rank 0 inside the timed region
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -244,7 +248,7 @@ def main():
                        "rays_per_step": int(per_step_rays),
                        "parallelism": ("rows %d:%d (band)" % band) if band else
                                       ("frame-per-gpu%d" % world) if args.scaling == "weak"
-                                      else "rows%d-%s" % (world, args.shard),
+                                      else "rows%d-%s%s" % (world, args.shard, "-pipelined" if dr.pipeline else ""),
                        "kernel": "specialised" if spec_active else "generic",
                        "accel": "bvh+cull" if args.accel == "bvh" else "none (brute force)",
                        "spec_compile_ms": round(spec_ms, 1)},

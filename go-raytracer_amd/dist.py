@@ -78,6 +78,40 @@ def gather_frame(buf, height, mode="bands", group=None, collective=None):
     return None
 
 
+class PendingGather:
+    """An in-flight gather of one rank buffer (async_op): wait() completes it
+    and returns the assembled frame on rank 0 (None elsewhere)."""
+
+    def __init__(self, work, stacked, height, mode, shape):
+        self.work, self.stacked, self.height, self.mode, self.shape = work, stacked, height, mode, shape
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        if self.stacked is None:
+            return None
+        if self.mode == "interleaved":
+            return deinterleave(self.stacked, self.height)
+        return self.stacked.reshape(-1, *self.shape[1:])[:self.height].clone()
+
+
+def gather_frame_async(buf, height, mode, slot, group=None):
+    """gather_frame as an async collective into receive slot `slot` (one
+    receive tensor per slot on rank 0, so two frames can be in flight)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if dist.get_rank(group) == 0:
+        key = (tuple(buf.shape), buf.dtype, buf.device, world, "slot", slot)
+        stacked = _recv.get(key)
+        if stacked is None:
+            stacked = _recv[key] = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+        work = dist.gather(buf, gather_list=list(stacked.unbind(0)), dst=0, group=group, async_op=True)
+        return PendingGather(work, stacked, height, mode, tuple(buf.shape))
+    return PendingGather(dist.gather(buf, dst=0, group=group, async_op=True), None, height, mode, tuple(buf.shape))
+
+
 def reduce_max_sum(values, device=None):
     """(max over ranks, sum over ranks) of a list of floats (one all_reduce
     each; identity without an initialised process group). Used for the step
@@ -98,7 +132,7 @@ class DistributedRenderer:
     share of one frame's rows ("interleaved" / "bands", strong scaling) followed
     by the gather to rank 0."""
 
-    def __init__(self, ctx, packed, rank, world, device, mode="interleaved", band=None):
+    def __init__(self, ctx, packed, rank, world, device, mode="interleaved", band=None, pipeline=False):
         import torch
         self.ctx = ctx
         self.packed = packed
@@ -127,6 +161,14 @@ class DistributedRenderer:
             self.y0, self.y1, rows = band_rows(self.H, rank, world)
         self.buf = torch.zeros((rows, self.W, 4), dtype=torch.uint8, device=device)
         self.frame = None
+        # pipeline (strong scaling over >1 rank): two rank buffers alternate and
+        # each gather runs asynchronously, so frame k's gather overlaps frame
+        # k+1's render; a buffer is reused only after its gather has completed
+        # (pipeline="always": also at one rank -- the GPU test of the RCCL path)
+        self.pipeline = (pipeline == "always" or (bool(pipeline) and world > 1)) and mode in ("interleaved", "bands")
+        self.bufs = [self.buf, torch.zeros_like(self.buf)] if self.pipeline else [self.buf]
+        self.pending = [None] * len(self.bufs)
+        self.k = 0
 
     def has_work(self):
         if self.mode in ("frame", "band"):
@@ -148,14 +190,33 @@ class DistributedRenderer:
                 events[1].record()
             self.frame = self.buf  # rank-local rows; nothing to exchange
             return self.frame
+        slot = self.k % len(self.bufs)
+        self.k += 1
+        if self.pending[slot] is not None:  # this buffer's previous gather must be done
+            self.frame = self.pending[slot].wait()
+            self.pending[slot] = None
+        buf = self.bufs[slot]
         if self.mode == "interleaved":
             if self.ntrows > 0:
                 self.ctx.render_tile_rows_async(self.rank, self.world, self.ntrows,
-                                                self.buf[: self.ntrows * TILE])
+                                                buf[: self.ntrows * TILE])
         elif self.y1 > self.y0:
-            self.ctx.render_rows_async(self.y0, self.y1, self.buf[: self.y1 - self.y0])
+            self.ctx.render_rows_async(self.y0, self.y1, buf[: self.y1 - self.y0])
         if events is not None:
             events[1].record()
         if gather:
-            self.frame = gather_frame(self.buf, self.H, self.mode, collective=collective)
+            if self.pipeline:
+                self.pending[slot] = gather_frame_async(buf, self.H, self.mode, slot)
+                return None  # the frame comes from flush() / a later step
+            self.frame = gather_frame(buf, self.H, self.mode, collective=collective)
+        return self.frame
+
+    def flush(self):
+        """Complete every in-flight gather (pipeline mode); returns the frame of
+        the last step on rank 0."""
+        order = [(self.k + i) % len(self.bufs) for i in range(len(self.bufs))]  # oldest first
+        for slot in order:
+            if self.pending[slot] is not None:
+                self.frame = self.pending[slot].wait()
+                self.pending[slot] = None
         return self.frame

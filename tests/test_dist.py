@@ -98,6 +98,15 @@ class _OracleCtx:
         img, _ = self.ob.render_rows(self.packed, y0, y1, threads=2)
         out[: y1 - y0] = torch.from_numpy(img)
 
+    def render_tile_rows_async(self, trow0, stride, ntrows, out, stream=None):
+        h = self.packed.height
+        for j in range(ntrows):
+            y0 = (trow0 + j * stride) * 8
+            y1 = min(h, y0 + 8)
+            if y1 > y0:
+                img, _ = self.ob.render_rows(self.packed, y0, y1, threads=2)
+                out[j * 8: j * 8 + (y1 - y0)] = torch.from_numpy(img)
+
 
 def _weak_worker(rank, world, port, w, h, q):
     import sys
@@ -146,3 +155,56 @@ def test_weak_scaling_frame_per_rank():
 def test_reduce_max_sum_without_process_group():
     import go_raytracer_amd as rt
     assert rt.dist.reduce_max_sum([1.5, 2.0]) == ([1.5, 2.0], [1.5, 2.0])
+
+
+def _pipeline_worker(rank, world, port, w, h, q, mode):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    import oracle_bind
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    packed = pkg.scene.convert(pkg.configs.c2(width=w, height=h))
+    dr = pkg.dist.DistributedRenderer(_OracleCtx(packed, oracle_bind), packed, rank, world, "cpu", mode=mode,
+                                      pipeline=True)
+    assert dr.pipeline and len(dr.bufs) == 2
+    frames = []
+    for _ in range(3):  # step 3 reuses step 1's buffer: its gather completes first
+        dr.step()
+        if dr.frame is not None:
+            frames.append(dr.frame.numpy().copy())
+    last = dr.flush()
+    if rank == 0:
+        frames.append(last.numpy().copy())
+        q.put(frames)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "interleaved"), (3, "bands")])
+def test_pipelined_gather_frames_equal_full_frame(world, mode):
+    """bench.py --scaling strong over several ranks: two rank buffers alternate
+    and each gather is asynchronous (frame k's gather overlaps frame k+1's
+    render); every gathered frame equals the full-frame render."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind
+    import go_raytracer_amd as rt
+    w, h = 48, 36
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, w, h, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full, _ = oracle_bind.render_rows(rt.scene.convert(rt.configs.c2(width=w, height=h)))
+    assert len(frames) == 2  # step 3 completed step 1's gather; flush the last one
+    for f in frames:
+        assert np.array_equal(f, full)

@@ -55,6 +55,32 @@ def test_rccl_gathered_frame_equals_full_render(nccl_group, mode):
         ctx.close()
 
 
+@pytest.mark.parametrize("mode", ["interleaved", "bands"])
+def test_rccl_pipelined_gathers_equal_full_render(nccl_group, mode):
+    """bench.py's strong-scaling loop: two rank buffers alternate, each RCCL
+    gather is asynchronous and completes at the buffer's next use or flush()."""
+    import torch
+    packed = rt.scene.convert(rt.configs.c3(width=320, height=180))
+    ctx = rt.RenderContext(0)
+    try:
+        ctx.set_scene(packed)
+        full = ctx.render()
+        dr = rt.dist.DistributedRenderer(ctx, packed, 0, 1, torch.device("cuda", 0), mode=mode, pipeline="always")
+        assert dr.pipeline
+        got = []
+        for _ in range(3):
+            dr.step()
+            if dr.frame is not None:
+                got.append(dr.frame.cpu().numpy())
+        got.append(dr.flush().cpu().numpy())
+        torch.cuda.synchronize()
+        assert len(got) == 2
+        for g in got:
+            assert np.array_equal(g, full)
+    finally:
+        ctx.close()
+
+
 def test_rccl_max_sum_reduction(nccl_group):
     import torch
     mx, sm = rt.dist.reduce_max_sum([1.5, 7.0], device=torch.device("cuda", 0))
