@@ -464,6 +464,7 @@ struct rt_context {
   int last_waves = 0, launches = 0;  // diagnostics (RT_PHASE_TIMING wave lifetimes)
   int sched = RT_SCHED_AUTO;         // rt_set_schedule
   LaunchPlan plan;                   // last launch's occupancy / LDS plan
+  unsigned long long* wdiag = nullptr;  // diagnostic build: per-wave lifetimes (RT_PHASE_TIMING)
   int cus = 0;
   int lds_per_cu = 0, lds_per_block = 0;  // bytes (device properties)
   int grid_lds = 0, grid_glb = 0;  // persistent grids (workgroups) per kernel flavour
@@ -1536,6 +1537,11 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.jump = c->jump;
   P.queue = c->queue;
   P.stats = c->stats;
+#ifdef RT_PHASE_TIMING
+  if (!c->wdiag && hipMalloc((void**)&c->wdiag, sizeof(unsigned long long) * 4 * 8192) != hipSuccess) c->wdiag = nullptr;
+  if (c->wdiag) HIP_TRY(hipMemsetAsync(c->wdiag, 0, sizeof(unsigned long long) * 4 * 8192, st));
+  P.wdiag = c->wdiag;
+#endif
   P.stack = c->stack;
   P.out = (uint32_t*)d_rgba;
   P.width = s.width;
@@ -1640,6 +1646,25 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
       fprintf(stderr, " total_wave_cycles=%.4g\n", (double)tot);
       unsigned long long bd[8];
       HIP_TRY(hipMemcpy(bd, c->stats + ST_BVHDIAG, sizeof bd, hipMemcpyDeviceToHost));
+      if (c->wdiag && c->last_waves > 0) {
+        // last launch: lifetime percentiles, and the longest waves' last chunk
+        std::vector<unsigned long long> w((size_t)c->last_waves * 4);
+        HIP_TRY(hipMemcpy(w.data(), c->wdiag, w.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        std::vector<std::pair<unsigned long long, int>> life;
+        for (int i = 0; i < c->last_waves; i++) life.push_back({w[(size_t)i * 4], i});
+        std::sort(life.begin(), life.end());
+        auto pct = [&](double q) { return (double)life[std::min(life.size() - 1, (size_t)(q * life.size()))].first; };
+        fprintf(stderr, "[tail] lifetime p10 %.4g p50 %.4g p90 %.4g p99 %.4g max %.4g;", pct(0.1), pct(0.5), pct(0.9),
+                pct(0.99), (double)life.back().first);
+        for (int k = 1; k <= 4 && k <= (int)life.size(); k++) {
+          const int i = life[life.size() - k].second;
+          fprintf(stderr, " [life %.4g chunks %llu last-chunk %.4g]", (double)w[(size_t)i * 4], w[(size_t)i * 4 + 1],
+                  (double)w[(size_t)i * 4 + 2]);
+        }
+        double lc = 0;
+        for (int i = 0; i < c->last_waves; i++) lc += (double)w[(size_t)i * 4 + 2];
+        fprintf(stderr, " mean last-chunk %.4g\n", lc / c->last_waves);
+      }
       fprintf(stderr, "[waves] lifetime mean %.4g cycles, max %.4g cycles (mean/max %.3f)\n",
               (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches), (double)bd[7],
               (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches) / (double)std::max(1ull, bd[7]));

@@ -150,6 +150,7 @@ struct Params {
   const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
   unsigned int* queue;
   unsigned long long* stats;
+  unsigned long long* wdiag;  // diagnostic build: per wave [lifetime, chunks, cycles since last chunk grab, 0]
   double* stack;
   uint32_t* out;
   int width, height, depth, nobj, nlights, y0, y1, tiles_x;
@@ -1409,6 +1410,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   PH_BEGIN();
 #ifdef RT_PHASE_TIMING
   const uint64_t life_t0 = ph_t0_;
+  uint64_t last_grab = life_t0, nchunk_taken = 0;
 #endif
   for (;;) {
     // ---- quads whose 4 samples are all done: the first lane adds the
@@ -1458,6 +1460,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           exhausted = true;
           break;
         }
+#ifdef RT_PHASE_TIMING
+        last_grab = stamp();
+        nchunk_taken++;
+#endif
         pool_next = c * QCHUNK;
         pool_end = min(pool_next + (unsigned int)QCHUNK, P.total_slots);
       }
@@ -2326,6 +2332,11 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     const uint64_t life = stamp() - life_t0;
     atomicAdd(P.stats + ST_BVHDIAG + 6, (unsigned long long)life);
     atomicMax(P.stats + ST_BVHDIAG + 7, (unsigned long long)life);
+    if (P.wdiag) {
+      P.wdiag[(size_t)wslot * 4 + 0] = life;
+      P.wdiag[(size_t)wslot * 4 + 1] = nchunk_taken;
+      P.wdiag[(size_t)wslot * 4 + 2] = stamp() - last_grab;
+    }
 #endif
   }
   // Workgroup reduction of the per-lane counters (every wave of the group
