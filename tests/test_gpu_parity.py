@@ -686,3 +686,29 @@ def test_pixel_quads_and_serial_samples_match_oracle(ctx, spec_ctx, case):
     finally:
         for c in (ctx, spec_ctx):
             c.set_schedule(rt.abi.RT_SCHED_AUTO)
+
+
+# --- full-size frames of the BASELINE configs, byte for byte and counter for
+# counter against the oracle (its threads on every CPU this job may use).
+# C5 (7680x4320 with 100k spheres) is beyond the oracle's reach here; its
+# parity rests on the bands above.
+
+def _oracle_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 8
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(n, 32))
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c3cone", "c4", "c4csg"])
+def test_full_size_config_matches_oracle(ctx, spec_ctx, name):
+    packed = rt.scene.convert(rt.configs.CONFIGS[name]())
+    ref, ost = oracle_bind.render_rows(packed, threads=_oracle_threads())
+    for c in (ctx, spec_ctx):
+        img, st = render(c, packed)
+        assert_same(img, ref, "full-size %s" % name)
+        assert st.as_dict() == ost.as_dict()
