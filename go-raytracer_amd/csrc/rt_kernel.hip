@@ -1615,9 +1615,14 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
   if (!c || !out) return fail(RT_E_INVALID, "rt_read_stats: NULL argument");
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
-  unsigned long long h[ST_COUNT];
+  unsigned long long h[ST_COUNT], wd = 0;
   HIP_TRY(hipMemcpyAsync(h, c->stats, sizeof h, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&wd, c->stats + ST_WATCHDOG, sizeof wd, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (wd) {
+    if (reset) (void)hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st);
+    return fail(RT_E_DEVICE, "render watchdog: " + std::to_string(wd) + " waves stopped unfinished (kernel bug)");
+  }
   std::memset(out, 0, sizeof *out);
   // Intersect calls from closestHit: every traced ray tests every object.
   uint64_t per_kind[RT_NUM_KINDS] = {0, 0, 0, 0, 0};

@@ -129,7 +129,7 @@ enum { QHEADS = 8, QSTRIDE = 16 /* u32 between heads: 64 B */ };
 #endif
 enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
-       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32 };  // (stats buffer: 64 entries)
+       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32, ST_WATCHDOG = 63 };  // (stats buffer: 64 entries)
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };  // S_DONE: sample colour held for the quad
 #ifndef RT_LDS_MAX
 #define RT_LDS_MAX (40 * 1024)
@@ -1412,7 +1412,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   const uint64_t life_t0 = ph_t0_;
   uint64_t last_grab = life_t0, nchunk_taken = 0;
 #endif
+  uint32_t guard_iters = 0;
   for (;;) {
+    // watchdog: a wave that has not finished after 2^26 scheduling rounds
+    // (far beyond any frame) stops and reports instead of hanging the device
+    if (++guard_iters > (1u << 26)) {
+      if (lane == 0) atomicAdd(P.stats + ST_WATCHDOG, 1ull);
+      break;
+    }
     // ---- quads whose 4 samples are all done: the first lane adds the
     // colours in sample order (raytracer.go:651) and quantises
     // (raytracer.go:656, vec.go:104-107); the quad becomes idle ----
