@@ -1,0 +1,45 @@
+"""The executed-work roofline fields bench.py reports come from committed
+rocprofv3 PMC summaries (profiles/pmc_<config>.json, scripts/pmc_roofline.py).
+Recompute them from the committed raw counter CSVs and check the summaries
+(and the bench's reader) against that -- the numbers are reproducible from the
+files, as DESIGN.md §4 says."""
+import glob
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("name", ["pmc_c3", "pmc_c5_bf_rows2048-2304"])
+def test_pmc_summary_recomputes_from_committed_csvs(tmp_path, name):
+    ref = json.load(open(os.path.join(ROOT, "profiles", name + ".json")))
+    srcs = [os.path.join(ROOT, f) for f in ref["source"]]
+    assert srcs and all(os.path.exists(f) for f in srcs), ref["source"]
+    pattern = os.path.join(os.path.dirname(srcs[0]), os.path.basename(srcs[0]).split("_p")[0] + "_p[12]_*.csv")
+    assert sorted(glob.glob(pattern)) == sorted(srcs)
+    out = tmp_path / "pmc.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_roofline.py"), pattern, str(out), "rt_render"],
+                   check=True, capture_output=True, cwd=ROOT)
+    got = json.load(open(out))
+    for k in ("executed_fp64_flops", "lane_util", "fp64_pipe_busy", "valu_busy", "issue_util"):
+        assert got[k] == pytest.approx(ref[k], rel=1e-12), k
+    # the definitions: FP64 ops x 64 lanes x lane utilisation; 4-cycle wave64 FP64 ops over 1024 SIMDs
+    c = got["counters"]
+    f64 = c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_TRANS_F64"] + \
+        2 * c["SQ_INSTS_VALU_FMA_F64"]
+    assert got["executed_fp64_flops"] == pytest.approx(f64 * 64 * got["lane_util"], rel=1e-12)
+    simd_cycles = 1024 * c["GRBM_GUI_ACTIVE"] / 8
+    assert got["valu_busy"] == pytest.approx(c["SQ_ACTIVE_INST_VALU"] * 4 / simd_cycles, rel=1e-12)
+
+
+def test_bench_reads_the_committed_summary():
+    sys.path.insert(0, ROOT)
+    import bench
+    ex, src = bench.pmc_executed("c3")
+    assert src == os.path.join("profiles", "pmc_c3.json")
+    assert ex["executed_fp64_flops"] > 1e10 and 0 < ex["issue_util"] < 1.5
+    assert bench.pmc_executed("no_such_config") == (None, None)
