@@ -1479,25 +1479,31 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                                    : __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
       unsigned int take = min((unsigned int)__popcll(mask), pool_end - pool_next);
+      // a pool never crosses a tile: the tile's position is wave-uniform
+      const unsigned int tile = pool_next / (TILE * TILE);
+      const int trow = (int)(tile / (unsigned)P.tiles_x);
+      const int x0 = (int)((tile % (unsigned)P.tiles_x) * TILE);
+      const int orow0 = trow * TILE;
+      const int y0t = P.trow_stride > 0 ? (P.trow0 + trow * P.trow_stride) * TILE : P.y0 + orow0;
+      const int r0t = y0t % 20;  // the tile's first row within its 20-row strip
       if (need && rank < take) {
-        unsigned int slot = pool_next + rank;
-        unsigned int tile = slot / (TILE * TILE), within = slot % (TILE * TILE);
+        const unsigned int within = pool_next % (TILE * TILE) + rank;
         // quads: a 16-pixel chunk is a 4x4 quarter of the tile
         const int tx = QD ? (int)(((within >> 4) & 1u) * 4u + (within & 3u)) : (int)(within % TILE);
         const int ty = QD ? (int)((within >> 5) * 4u + ((within >> 2) & 3u)) : (int)(within / TILE);
-        const int trow = (int)(tile / (unsigned)P.tiles_x);
-        const int x = (int)((tile % (unsigned)P.tiles_x) * TILE + tx);
-        const int orow = trow * TILE + ty;
-        const int y = P.trow_stride > 0 ? (P.trow0 + trow * P.trow_stride) * TILE + ty : P.y0 + orow;
+        const int x = x0 + tx;
+        const int orow = orow0 + ty;
+        const int y = y0t + ty;
         if (x < P.width && y < P.y1) {
           px = x;
           py = y;
           pout = (unsigned int)orow * (unsigned int)P.width + (unsigned int)x;
           // rng = PCG(0xDEAD^x, 0xBEEF^ymin) advanced 8*(y%20) draws
           // (raytracer.go:632-643: 2 draws per sample, 4 samples per row).
-          int ymin = y - y % 20;
+          const int ry = r0t + ty >= 20 ? r0t + ty - 20 : r0t + ty;  // y % 20 (ty < 8)
+          const int ymin = y - ry;
           Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
-          const uint64_t* j = jtab + (y % 20) * 4;
+          const uint64_t* j = jtab + ry * 4;
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sample = QD ? (lane & 3) : 0;
           if constexpr (QD) rng = pcg_skip_samples(rng, sample);
