@@ -1670,6 +1670,14 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
         for (int i = 0; i < c->last_waves; i++) lc += (double)w[(size_t)i * 4 + 2];
         fprintf(stderr, " mean last-chunk %.4g\n", lc / c->last_waves);
       }
+#ifdef RT_CSG_DIAG
+      {
+        unsigned long long cd[4] = {0, 0, 0, 0};
+        if (hipMemcpyFromSymbol(cd, HIP_SYMBOL(g_csg_diag), sizeof cd) == hipSuccess && cd[0])
+          fprintf(stderr, "[csg] searches %llu, register-list overflows %llu (%.2f%%), mean live leaves %.2f\n", cd[0],
+                  cd[1], 100.0 * cd[1] / cd[0], (double)cd[2] / cd[0]);
+      }
+#endif
       fprintf(stderr, "[waves] lifetime mean %.4g cycles, max %.4g cycles (mean/max %.3f)\n",
               (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches), (double)bd[7],
               (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches) / (double)std::max(1ull, bd[7]));

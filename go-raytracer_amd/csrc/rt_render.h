@@ -820,6 +820,11 @@ __device__ __forceinline__ bool csg_hit_all(const double* geo, const int* kinds,
   }
 }
 
+#ifdef RT_CSG_DIAG
+__device__ unsigned long long g_csg_diag[4];  // diagnostic build: searches, overflows, live leaves
+#undef RT_CSG_DIAG
+#define RT_CSG_DIAG g_csg_diag
+#endif
 // The same search over a register-resident list of the live leaves (at most
 // RT_CSG_LIVE per lane, ascending leaf order, so every tie breaks as above):
 // a ray meets only a few of a composite's leaves, and the per-lane interval
@@ -870,6 +875,11 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
       n++;
     }
   }
+#ifdef RT_CSG_DIAG
+  atomicAdd(RT_CSG_DIAG + 0, 1ull);  // composite searches
+  if (n > K) atomicAdd(RT_CSG_DIAG + 1, 1ull);  // ... that overflowed the register list
+  atomicAdd(RT_CSG_DIAG + 2, (unsigned long long)n);  // live leaves
+#endif
   if (n > K) return csg_hit_all_call(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
   double tc = 0.0;
   for (;;) {
