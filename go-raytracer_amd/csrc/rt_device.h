@@ -450,16 +450,6 @@ __device__ __forceinline__ Pcg pcg_jump(Pcg s, uint64_t ahi, uint64_t alo, uint6
   return Pcg{hi, lo2};
 }
 
-// 2k further LCG steps (k = 0..3: the draws of a pixel's samples before
-// sample k, raytracer.go:642-643), from constant jump tables.
-__device__ __forceinline__ Pcg pcg_skip_samples(Pcg s, int k) {
-  const uint64_t ahi = k == 1 ? 0x17bce35bdf69743cULL : (k == 2 ? 0xf4dd417327db7a9bULL : (k == 3 ? 0x19b2add48defcda8ULL : 0ULL));
-  const uint64_t alo = k == 1 ? 0x529ed9eb20e0ae99ULL : (k == 2 ? 0xd194dfbe42d45771ULL : (k == 3 ? 0x81ab1c97e7371089ULL : 1ULL));
-  const uint64_t chi = k == 1 ? 0x4871bec9994273f8ULL : (k == 2 ? 0x93d2c4665cea0ea8ULL : (k == 3 ? 0x283645fca186e3c6ULL : 0ULL));
-  const uint64_t clo = k == 1 ? 0xac1f8a1c3883459aULL : (k == 2 ? 0xca268d515f068aa4ULL : (k == 3 ? 0x64098dee4527999eULL : 0ULL));
-  return pcg_jump(s, ahi, alo, chi, clo);
-}
-
 // int64(v) for float64 v on amd64 (CVTTSD2SQ): MinInt64 on NaN/overflow.
 __device__ __forceinline__ long long go_f2i(double v) {
   if (!(v >= -9223372036854775808.0 && v < 9223372036854775808.0)) return (long long)0x8000000000000000ULL;

@@ -946,20 +946,22 @@ int rt_create(int device, rt_context** out) {
       per_cu <= 0)
     per_cu = 2;
   c->grid_glb = c->cus * std::min(per_cu, 8);
-  // PCG jump table: 8*r LCG steps, r = 0..19 (pcg.go: mul/inc constants).
-  std::vector<uint64_t> jump(20 * 4);
+  // PCG jump table: entry (r, k) = 8*r + 2*k LCG steps (pcg.go: mul/inc
+  // constants), r = 0..19 the row within its 20-row strip, k = 0..3 the
+  // sample (its first draw, raytracer.go:642-643) -- one jump per sample.
+  std::vector<uint64_t> jump(JUMP_ENTRIES * 4);
   {
     typedef unsigned __int128 u128;
     const u128 mul = ((u128)2549297995355413924ULL << 64) | 4865540595714422341ULL;
     const u128 inc = ((u128)6364136223846793005ULL << 64) | 1442695040888963407ULL;
     u128 A = 1, Cc = 0;
-    for (int step = 0; step <= 8 * 19; step++) {
-      if (step % 8 == 0) {
-        int r = step / 8;
-        jump[r * 4 + 0] = (uint64_t)(A >> 64);
-        jump[r * 4 + 1] = (uint64_t)A;
-        jump[r * 4 + 2] = (uint64_t)(Cc >> 64);
-        jump[r * 4 + 3] = (uint64_t)Cc;
+    for (int step = 0; step < 2 * JUMP_ENTRIES; step++) {
+      if (step % 2 == 0) {
+        const int e = step / 2;  // = 4*r + k
+        jump[e * 4 + 0] = (uint64_t)(A >> 64);
+        jump[e * 4 + 1] = (uint64_t)A;
+        jump[e * 4 + 2] = (uint64_t)(Cc >> 64);
+        jump[e * 4 + 3] = (uint64_t)Cc;
       }
       A = A * mul;
       Cc = Cc * mul + inc;
@@ -1449,7 +1451,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * 12 : 0);
   const int jump_off = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
   // per-wave object-record stream buffers (global linear scenes, RT_STREAM)
-  const int stream_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);
+  const int stream_off = jump_off + JUMP_ENTRIES * 4 * (int)sizeof(uint64_t);
   // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
   // loads instead: no stream buffers)
   // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)

@@ -135,6 +135,8 @@ enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };  // S_DONE: sample co
 #define RT_LDS_MAX (40 * 1024)
 #endif
 enum { LDS_MAX_BYTES = RT_LDS_MAX };
+// PCG jump table entries: (row within the 20-row strip) x (sample 0..3)
+enum { JUMP_ENTRIES = 20 * 4 };
 
 struct Params {
   int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
@@ -1168,7 +1170,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // Stage the PCG jump table (and, LDS flavour, the whole scene) once per
   // workgroup (the only block-wide barrier).
   uint64_t* jtab = reinterpret_cast<uint64_t*>(smem + P.jump_off);
-  if (threadIdx.x < 20 * 4) jtab[threadIdx.x] = P.jump[threadIdx.x];
+  for (int i = threadIdx.x; i < JUMP_ENTRIES * 4; i += WG) jtab[i] = P.jump[i];
   if constexpr (LDS) {
     const int n16 = P.blob_bytes / 16;
     for (int i = threadIdx.x; i < n16; i += WG)
@@ -1508,15 +1510,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           px = x;
           py = y;
           pout = (unsigned int)orow * (unsigned int)P.width + (unsigned int)x;
-          // rng = PCG(0xDEAD^x, 0xBEEF^ymin) advanced 8*(y%20) draws
-          // (raytracer.go:632-643: 2 draws per sample, 4 samples per row).
+          // rng = PCG(0xDEAD^x, 0xBEEF^ymin) advanced 8*(y%20) + 2*sample
+          // draws (raytracer.go:632-643: 2 draws per sample, 4 samples per row)
           const int ry = r0t + ty >= 20 ? r0t + ty - 20 : r0t + ty;  // y % 20 (ty < 8)
           const int ymin = y - ry;
           Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
-          const uint64_t* j = jtab + ry * 4;
-          rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sample = QD ? (lane & 3) : 0;
-          if constexpr (QD) rng = pcg_skip_samples(rng, sample);
+          const uint64_t* j = jtab + (ry * 4 + sample) * 4;
+          rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sum = mk(0, 0, 0);
           sp = 0;
           need_gen = true;
