@@ -471,7 +471,8 @@ struct rt_context {
   DevScene sc;
   bool has_scene = false;
   uint64_t* jump = nullptr;
-  unsigned int* queue = nullptr;
+  unsigned int* queue = nullptr;  // two sets of QHEADS queue heads (launches alternate)
+  int qset = 0;                    // the set the next launch dequeues from
   unsigned long long* stats = nullptr;
   double* stack = nullptr;
   double* vm_global = nullptr;  // per-lane VM material records (global flavour)
@@ -968,7 +969,10 @@ int rt_create(int device, rt_context** out) {
     }
   }
   int rc = upload(&c->jump, jump);
-  if (rc == RT_OK && hipMalloc((void**)&c->queue, 512) != hipSuccess) rc = fail(RT_E_NOMEM, "queue alloc");
+  if (rc == RT_OK && hipMalloc((void**)&c->queue, 2 * QSET * sizeof(unsigned int)) != hipSuccess)
+    rc = fail(RT_E_NOMEM, "queue alloc");
+  if (rc == RT_OK && hipMemset(c->queue, 0, 2 * QSET * sizeof(unsigned int)) != hipSuccess)
+    rc = fail(RT_E_DEVICE, "queue memset");
   if (rc == RT_OK && hipMalloc((void**)&c->stats, sizeof(unsigned long long) * 64) != hipSuccess)
     rc = fail(RT_E_NOMEM, "stats alloc");
   if (rc == RT_OK && hipMemset(c->stats, 0, sizeof(unsigned long long) * 64) != hipSuccess)
@@ -1445,13 +1449,14 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   hipStream_t st = (hipStream_t)stream;
   const bool lds = scene_in_lds(s);
   // Dynamic LDS: [scene blob (LDS flavour)] [VM records] [BVH stack]
-  // [counters] [PCG jump table] [frame cores of the first lds_levels levels]
+  // [counters] [drained-head mask] [PCG jump rows] [frame cores of the first lds_levels levels]
   const int vm_off = lds ? s.blob_bytes : 0;
   const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
   const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * 12 : 0);
-  const int jump_off = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
+  const int qmask_off = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
   // per-wave object-record stream buffers (global linear scenes, RT_STREAM)
-  const int stream_off = jump_off + JUMP_ENTRIES * 4 * (int)sizeof(uint64_t);
+  const int jump_off = qmask_off + 16;  // after the drained-head mask: the sample-0 jump rows
+  const int stream_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);
   // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
   // loads instead: no stream buffers)
   // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)
@@ -1521,6 +1526,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.lds_full = lds_full;
   P.stream_off = stream_off;
   P.lds_ext_off = ext_off;
+  P.qmask_off = qmask_off;
   P.jump_off = jump_off;
   P.off_geo = s.off_geo;
   P.off_shade = s.off_shade;
@@ -1537,7 +1543,10 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.vm_global = c->vm_global;
   P.blob_bytes = s.blob_bytes;
   P.jump = c->jump;
-  P.queue = c->queue;
+  // this launch dequeues from set qset and zeroes the other set for the next
+  // one (launches on a context are stream-ordered): no memset per launch
+  P.queue = c->queue + c->qset * QSET;
+  P.queue_next = c->queue + (1 - c->qset) * QSET;
   P.stats = c->stats;
 #ifdef RT_PHASE_TIMING
   if (!c->wdiag && hipMalloc((void**)&c->wdiag, sizeof(unsigned long long) * 4 * 8192) != hipSuccess) c->wdiag = nullptr;
@@ -1574,7 +1583,6 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     P.bvh_stack_off = stack_off;
   }
 
-  HIP_TRY(hipMemsetAsync(c->queue, 0, 512, st));  // QHEADS queue heads, 64 B apart
   HIP_TRY(hipEventRecord(c->ev0, st));
   const char* blob = s.blob;
   void* args[] = {(void*)&blob, (void*)&P};
@@ -1583,6 +1591,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   else
     HIP_TRY(hipLaunchKernel(kfn, dim3(grid), dim3(WG), args, shmem, st));
   HIP_TRY(hipGetLastError());
+  c->qset ^= 1;
   HIP_TRY(hipEventRecord(c->ev1, st));
   c->timed = true;
   uint64_t rows = 0;

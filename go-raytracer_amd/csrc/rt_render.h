@@ -120,10 +120,23 @@ enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM mat
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
 // Work queue: pixels per dequeue -- one 8x8 tile, or with pixel quads a 4x4
 // quarter of one (16 quads = one wave's lanes) -- from QHEADS queue heads
-// (chunk c belongs to head c mod QHEADS; a workgroup starts on head blockIdx
-// mod QHEADS and moves to the others once it is drained), so the dequeue rate
+// (chunk c belongs to head c mod QHEADS; a workgroup dequeues from head
+// blockIdx mod QHEADS, see RT_QSTEAL), so the dequeue rate
 // stays below what one atomic word sustains.
 enum { QHEADS = 8, QSTRIDE = 16 /* u32 between heads: 64 B */ };
+// Heads a workgroup dequeues from: its home head, then RT_QSTEAL others once
+// that is drained. Every head is drained by its home workgroups, so stopping
+// early never drops a chunk; it bounds the end-of-launch probes (each a
+// returning atomic, serialised per head address: probing all 8 heads from
+// every wave cost ~45 us per launch). A workgroup shares the heads it found
+// drained through an LDS mask. One steal head: C3/C4 whole frames as with
+// all 7, a one-tile-row launch 85 -> 37 us, C2 0.38 -> 0.33 ms
+// (profiles/r02/qsteal). Not kept: launch-wide drained flags read before
+// stealing (one line written by every overflowing wave: slower).
+#ifndef RT_QSTEAL
+#define RT_QSTEAL 1
+#endif
+enum { QSET = QHEADS * QSTRIDE /* u32 per launch set of heads */ };
 #ifndef RT_QCHUNK_PIXEL
 #define RT_QCHUNK_PIXEL 64  // pixels per dequeue without quads (a multiple of 16 dividing 64)
 #endif
@@ -144,13 +157,15 @@ struct Params {
   int lds_full;        // recursion levels whose other frame fields (3..11) live in LDS too
   int lds_ext_off;     // byte offset of those fields in dynamic LDS
   int stream_off;      // byte offset of the per-wave object-record stream buffers (global linear scenes)
-  int jump_off;        // byte offset of the LDS copy of the PCG jump table
+  int qmask_off;       // byte offset of the workgroup's drained-head mask in LDS
+  int jump_off;        // byte offset of the LDS copy of the sample-0 jump rows (serial samples)
   int off_geo, off_shade, off_mats, off_lights, off_kind, off_objmat, off_pref, off_csg, off_code, off_consts,
       off_entry, blob_bytes;
   int lds_vm_off;     // LDS byte offset of the per-lane VM material records (LDS flavour)
   double* vm_global;  // per-lane VM material records (global flavour)
-  const uint64_t* jump;  // [20][4] : ahi alo chi clo (8*r LCG steps)
-  unsigned int* queue;
+  const uint64_t* jump;  // [20 rows][4 samples][ahi alo chi clo]: 8*r + 2*k LCG steps
+  unsigned int* queue;       // this launch's QHEADS queue heads (zero at launch)
+  unsigned int* queue_next;  // the next launch's heads: zeroed here by block 0
   unsigned long long* stats;
   unsigned long long* wdiag;  // diagnostic build: per wave [lifetime, chunks, cycles since last chunk grab, 0]
   double* stack;
@@ -1167,10 +1182,19 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #endif
   constexpr unsigned int QCHUNK = QD ? 16u : (unsigned int)RT_QCHUNK_PIXEL;
   const char* base;
-  // Stage the PCG jump table (and, LDS flavour, the whole scene) once per
-  // workgroup (the only block-wide barrier).
-  uint64_t* jtab = reinterpret_cast<uint64_t*>(smem + P.jump_off);
-  for (int i = threadIdx.x; i < JUMP_ENTRIES * 4; i += WG) jtab[i] = P.jump[i];
+  // Stage the scene (LDS flavour) once per workgroup (the only block-wide
+  // barrier).
+  // PCG jump table: with quads every sample starts from entry (row, sample),
+  // read from HBM (2.5 KB, cache resident: a whole LDS copy cost C4 a
+  // workgroup per CU and C3 a level of LDS frame cores); serial samples start
+  // at sample 0, whose 20 rows are staged in LDS
+  uint64_t* jrows = reinterpret_cast<uint64_t*>(smem + P.jump_off);
+  if constexpr (!QD)
+    for (int i = threadIdx.x; i < 20 * 4; i += WG) jrows[i] = P.jump[(i >> 2) * 16 + (i & 3)];
+  // drained-head mask of this workgroup
+  unsigned int* qdrained = reinterpret_cast<unsigned int*>(smem + P.qmask_off);
+  if (threadIdx.x == 0) *qdrained = 0u;
+  if (blockIdx.x == 0 && threadIdx.x < QHEADS) atomicExch(P.queue_next + threadIdx.x * QSTRIDE, 0u);
   if constexpr (LDS) {
     const int n16 = P.blob_bytes / 16;
     for (int i = threadIdx.x; i < n16; i += WG)
@@ -1467,15 +1491,22 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if (pool_next >= pool_end) {
         const unsigned int nchunks = (P.total_slots + QCHUNK - 1) / QCHUNK;
         unsigned int c = nchunks;
-        while (qhead < QHEADS) {
+        const int nheads = gridDim.x >= QHEADS ? min(QHEADS, RT_QSTEAL + 1) : QHEADS;
+        while (qhead < nheads) {
           const unsigned int h = (blockIdx.x + qhead) % QHEADS;
+          const unsigned int dm = __builtin_amdgcn_readfirstlane(__atomic_load_n(qdrained, __ATOMIC_RELAXED));
+          if ((dm >> h) & 1u) {  // another wave of the group found it drained
+            qhead++;
+            continue;
+          }
           unsigned int n = 0;
           if (lane == 0) n = atomicAdd(P.queue + h * QSTRIDE, 1u);
           c = __builtin_amdgcn_readfirstlane(n) * QHEADS + h;
           if (c < nchunks) break;
+          if (lane == 0) atomicOr(qdrained, 1u << h);
           qhead++;  // this head is drained: try the next one
         }
-        if (qhead >= QHEADS) {
+        if (qhead >= nheads) {
           exhausted = true;
           break;
         }
@@ -1516,7 +1547,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const int ymin = y - ry;
           Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
           sample = QD ? (lane & 3) : 0;
-          const uint64_t* j = jtab + (ry * 4 + sample) * 4;
+          const uint64_t* j = QD ? P.jump + (ry * 4 + sample) * 4 : jrows + ry * 4;
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sum = mk(0, 0, 0);
           sp = 0;

@@ -2,7 +2,7 @@
 frame (interleaved 8-row tile rows, stride = world) for world = 1, 2, 4, 8, as
 bench.py --scaling strong would launch it on each rank (no collective here).
 efficiency(world) = t(1) / (world * t(world)).
-usage: python scripts/strong_emul.py [config] [steps]"""
+usage: python scripts/strong_emul.py [config] [steps]   (STRONG_WORLDS=1,2,4,8 by default)"""
 import json
 import os
 import sys
@@ -24,7 +24,8 @@ def main():
     ctx.set_scene(packed)
     out = {"config": cfg}
     t1 = None
-    for world in (1, 2, 4, 8):
+    worlds = [int(w) for w in os.environ.get("STRONG_WORLDS", "1,2,4,8").split(",")]
+    for world in worlds:
         dr = pkg.dist.DistributedRenderer(ctx, packed, 0, world, torch.device("cuda", 0), mode="interleaved")
         for _ in range(3):
             dr.step(gather=False)
