@@ -1,7 +1,8 @@
 """Strong-scaling rehearsal on ONE GPU: the kernel time of rank 0's share of a
 frame (interleaved 8-row tile rows, stride = world) for world = 1, 2, 4, 8, as
 bench.py --scaling strong would launch it on each rank (no collective here).
-efficiency(world) = t(1) / (world * t(world)).
+efficiency(world) = t(1) / (world * t(world)); with STRONG_ALL_RANKS=1 (default)
+every rank's share is timed too and w<N>_eff_max uses the slowest one.
 usage: python scripts/strong_emul.py [config] [steps]   (STRONG_WORLDS=1,2,4,8 by default)"""
 import json
 import os
@@ -25,8 +26,10 @@ def main():
     out = {"config": cfg}
     t1 = None
     worlds = [int(w) for w in os.environ.get("STRONG_WORLDS", "1,2,4,8").split(",")]
-    for world in worlds:
-        dr = pkg.dist.DistributedRenderer(ctx, packed, 0, world, torch.device("cuda", 0), mode="interleaved")
+    all_ranks = os.environ.get("STRONG_ALL_RANKS", "1") == "1"
+
+    def share_ms(rank, world):
+        dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, torch.device("cuda", 0), mode="interleaved")
         for _ in range(3):
             dr.step(gather=False)
         torch.cuda.synchronize()
@@ -35,11 +38,20 @@ def main():
         for k in range(steps):
             dr.step(gather=False, events=ev[k])
         torch.cuda.synchronize()
-        out["w%d_wall_ms" % world] = round((time.perf_counter() - t0) / steps * 1e3, 4)
-        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        wall = (time.perf_counter() - t0) / steps * 1e3
+        return sorted(a.elapsed_time(b) for a, b in ev)[steps // 2], wall
+
+    for world in worlds:
+        ms, wall = share_ms(0, world)
+        out["w%d_wall_ms" % world] = round(wall, 4)
         t1 = t1 or ms
         out["w%d_ms" % world] = round(ms, 4)
         out["w%d_eff" % world] = round(t1 / (world * ms), 3)
+        if all_ranks and world > 1:
+            # the driver's step time is the slowest rank's share, not rank 0's
+            mx = max([ms] + [share_ms(r, world)[0] for r in range(1, world)])
+            out["w%d_max_ms" % world] = round(mx, 4)
+            out["w%d_eff_max" % world] = round(t1 / (world * mx), 3)
     print(json.dumps(out), flush=True)
 
 
