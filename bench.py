@@ -37,8 +37,8 @@ METRIC = "Mrays/s (primary+shadow+reflect) at 4K depth=6; 1/2/4/8-GPU scaling"  
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c3")
     p.add_argument("--width", type=int, default=None)
     p.add_argument("--height", type=int, default=None)
