@@ -43,3 +43,26 @@ def test_bench_reads_the_committed_summary():
     assert src == os.path.join("profiles", "pmc_c3.json")
     assert ex["executed_fp64_flops"] > 1e10 and 0 < ex["issue_util"] < 1.5
     assert bench.pmc_executed("no_such_config") == (None, None)
+
+
+def test_committed_bench_line_keeps_the_contract():
+    """The committed round bench line (profiles/r02/final/bench_c3.json) has the
+    driver's fields, and its derived numbers agree with each other: value =
+    rays per step / ms per step, frac = achieved / peak, and the rocprofv3
+    average of the same command is within 5 % of the in-bench kernel time."""
+    import csv
+    d = json.load(open(os.path.join(ROOT, "profiles", "r02", "final", "bench_c3.json")))
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["dtype"] == "f64" and d["n_gpus"] == 1 and d["higher_is_better"] is True
+    assert "workload" in d["config"] and d["config"]["width"] == 3840 and d["config"]["height"] == 2160
+    assert d["value"] == pytest.approx(d["config"]["rays_per_step"] / d["ms_per_step"] / 1e3, rel=2e-3)
+    r = d["roofline"]
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3)
+    assert r["achieved"] == pytest.approx(r["flops_per_launch"] / (r["kernel_ms"] * 1e-3) / 1e12, rel=2e-3)
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
+    rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", "r02", "final", "kernel_stats_c3.csv"))))
+    k = next(row for row in rows if row["Name"].startswith("void rt_render_kernel"))
+    assert float(k["AverageNs"]) * 1e-6 == pytest.approx(r["kernel_ms"], rel=0.05)
