@@ -1171,7 +1171,11 @@ struct View {
 // running long after the rest (host choice per scene, rt_kernel.hip).
 template <bool LDS, bool BVH, bool CSG, bool QUADS>
 #ifndef RT_MIN_WAVES
+#if RT_CULL
 #define RT_MIN_WAVES 3  // 168 VGPRs -> 3 waves/SIMD (C3 on par with 4; C2 -10%, C4 (BVH) -4%)
+#else
+#define RT_MIN_WAVES 5  // brute force (scalar-load sweep): 5 waves/SIMD, C5 band -7..-14 % vs 3 (profiles/r02/minwaves_ab)
+#endif
 #endif
 __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char* __restrict__ blob, Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
