@@ -176,6 +176,7 @@ def main():
         ctx.set_accel(0)
     ctx.set_scene(packed)
     spec_active, spec_ms = ctx.specialized()
+    order_active, order_ms = ctx.tile_order_info()
     mode = "frame" if args.scaling == "weak" else args.shard
     band = None
     if args.rows:
@@ -251,7 +252,8 @@ def main():
                                       else "rows%d-%s%s" % (world, args.shard, "-pipelined" if dr.pipeline else ""),
                        "kernel": "specialised" if spec_active else "generic",
                        "accel": "bvh+cull" if args.accel == "bvh" else "none (brute force)",
-                       "spec_compile_ms": round(spec_ms, 1)},
+                       "spec_compile_ms": round(spec_ms, 1),
+                       "tile_order_ms": round(order_ms, 2) if order_active else None},
             "roofline": {"bound": "valu-fp64", "achieved": round(achieved_tf, 3), "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
                          "frac_nofma_ceiling": round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),

@@ -5,7 +5,8 @@ sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
-RT_ABI_VERSION = 2  # include/rt_abi.h
+RT_ABI_VERSION = 3  # include/rt_abi.h
+RT_EXP_AMD64_FMA, RT_EXP_AMD64, RT_EXP_PORTABLE = 0, 1, 2  # rt_scene.exp_mode
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -96,7 +97,7 @@ class rt_scene(C.Structure):
         ("num_programs", C.c_int32),
         ("program_code_words", C.c_int32),
         ("program_const_count", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("exp_mode", C.c_int32),  # RT_EXP_*
         ("ext_lights", C.POINTER(rt_light)),
         ("num_ext_lights", C.c_int32),
         ("reserved1", C.c_int32),

@@ -262,12 +262,97 @@ __device__ __noinline__ double go_log(double x) {
   return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
 }
 
+// math.Exp / math.Log as Go runs them on amd64 (exp_amd64.s, log_amd64.s),
+// op for op the oracle's go_exp_amd64 / go_log_amd64 (oracle/go_math.h has
+// the algorithm notes; recalled from the Go sources, parity unpinned by any
+// reference fixture). fma: the AVX2+FMA branch (fused reduction and series).
+__device__ __noinline__ double go_exp_amd64(double x, bool fma) {
+  const double LOG2E = 1.4426950408889634073599246810018920;
+  const double LN2U = 0.69314718055966295651160180568695068359375;
+  const double LN2L = 0.28235290563031577122588448175013436025525412068e-12;
+  const double T0 = 0.5, T1 = 1.0, T2 = 2.0, T3 = 1.6666666666666666667e-1, T4 = 4.1666666666666666667e-2,
+               T5 = 8.3333333333333333333e-3, T6 = 1.3888888888888888889e-3, T7 = 1.9841269841269841270e-4,
+               T8 = 2.4801587301587301587e-5;
+  const uint64_t bx = (uint64_t)__double_as_longlong(x);
+  if ((bx & ~(1ull << 63)) >= 0x7FF0000000000000ull) return bx == 0xFFF0000000000000ull ? 0.0 : x;
+  if (x > 7.09782712893384e+02) return __builtin_inf();
+  const double t = LOG2E * x;
+  const int e = (t > -2147483649.0 && t < 2147483648.0) ? (int)t : (int)0x80000000;  // CVTTSD2SL
+  const double fe = (double)e;
+  double r, p = T8;
+  if (fma) {
+    r = __builtin_fma(-fe, LN2U, x);
+    r = __builtin_fma(-fe, LN2L, r);
+    r = r * 0.0625;
+    p = __builtin_fma(r, p, T7);
+    p = __builtin_fma(r, p, T6);
+    p = __builtin_fma(r, p, T5);
+    p = __builtin_fma(r, p, T4);
+    p = __builtin_fma(r, p, T3);
+    p = __builtin_fma(r, p, T0);
+    p = __builtin_fma(r, p, T1);
+  } else {
+    r = x - LN2U * fe;
+    r = r - LN2L * fe;
+    r = r * 0.0625;
+    p = p * r + T7;
+    p = p * r + T6;
+    p = p * r + T5;
+    p = p * r + T4;
+    p = p * r + T3;
+    p = p * r + T0;
+    p = p * r + T1;
+  }
+  double y = r * p;
+  for (int i = 0; i < 4; i++) y = y * (y + T2);
+  y = y + T1;
+  int b = e + 0x3FF;
+  if (b < 0) {
+    if (b < -52) return 0.0;
+    b += 0x3FE;
+    y = y * __longlong_as_double((long long)((uint64_t)(uint32_t)b << 52));
+    return y * __longlong_as_double((long long)(1ull << 52));
+  }
+  if ((uint32_t)b > 0x7FFu) return __builtin_inf();
+  return y * __longlong_as_double((long long)((uint64_t)(uint32_t)b << 52));
+}
+__device__ __noinline__ double go_log_amd64(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  const uint64_t bx = (uint64_t)__double_as_longlong(x);
+  if ((bx & ~(1ull << 63)) == 0) return -__builtin_inf();
+  if ((long long)bx < 0) return __builtin_nan("");
+  if (bx >= 0x7FF0000000000000ull) return x;
+  double f1 = __longlong_as_double((long long)((bx & 0x000FFFFFFFFFFFFFull) | 0x3FE0000000000000ull));
+  double k = (double)((int)((bx >> 52) & 0x7FF) - 0x3FE);
+  if (f1 < 0.70710678118654752440) {
+    f1 *= 2;
+    k -= 1;
+  }
+  const double f = f1 - 1;
+  const double s = f / (2 + f);
+  const double s2 = s * s;
+  const double s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2;
+  const double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+// RT_EXP_* (include/rt_abi.h): 0 amd64 with FMA, 1 amd64, 2 portable.
+__device__ __forceinline__ double go_exp_mode(double x, int mode) {
+  return mode == 2 ? go_exp(x) : go_exp_amd64(x, mode == 0);
+}
+__device__ __forceinline__ double go_log_mode(double x, int mode) { return mode == 2 ? go_log(x) : go_log_amd64(x); }
+
 // math.Pow (Go pow.go): special cases, then Frexp + repeated squaring with
 // mantissa renormalisation and a final Ldexp. Integer exponents (the
 // reference's specular n and Schlick's 5) are reproduced exactly; the
-// fractional part is go_exp(yf * go_log(x)), restated identically here and in
-// the oracle.
-__device__ __noinline__ double go_pow_general(double x, double y) {
+// fractional part is Exp(yf * Log(x)) of the platform `mode` selects
+// (go_exp_mode), restated identically here and in the oracle.
+__device__ __noinline__ double go_pow_general(double x, double y, int mode) {
   if (y == 0 || x == 1) return 1;
   if (y == 1) return x;
   if (__builtin_isnan(x) || __builtin_isnan(y)) return __builtin_nan("");
@@ -307,7 +392,7 @@ __device__ __noinline__ double go_pow_general(double x, double y) {
       yf--;
       yi++;
     }
-    a1 = go_exp(yf * go_log(x));
+    a1 = go_exp_mode(yf * go_log_mode(x, mode), mode);
   }
   int xe;
   double x1 = frexp(x, &xe);
@@ -344,7 +429,7 @@ __device__ __noinline__ double go_pow_general(double x, double y) {
 #ifndef RT_POW_DIRECT
 #define RT_POW_DIRECT 1  // exact direct binary powering for small integer exponents (see go_pow)
 #endif
-__device__ __forceinline__ double go_pow(double x, double y) {
+__device__ __forceinline__ double go_pow(double x, double y, int mode = 2) {
 #if RT_POW_DIRECT
   // Integer 2 <= y <= 64 and 2^-15 <= x <= 2^15: every power the loop below
   // forms (x^(2^k) for 2^k <= y, and the partial products, all between x^y and
@@ -389,7 +474,7 @@ __device__ __forceinline__ double go_pow(double x, double y) {
     return ldexp(a1, ae);
   }
   if (x == 0 && y > 0) return (signbit64(x) && go_is_odd_int(y)) ? x : 0.0;
-  return go_pow_general(x, y);
+  return go_pow_general(x, y, mode);
 }
 
 // go_pow's direct path without branches, for interleaving several powers:

@@ -247,7 +247,7 @@ struct DevScene {
   bool use_bvh = false;
   int nplanes = 0, nnodes = 0, kind_mask = 0;
   int light_mask = 0;  // bit k: the scene has lights of kind k (RT_LIGHT_*)
-  bool branching = false;  // some material is reflective and transparent (or a surface program decides)
+  bool branching = false;  // some material is reflective and transparent, or a surface program may make one
   int leaf_kind_mask = 0;  // bit k: some CSG leaf has kind k
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0;
   int nruns = 0;
@@ -484,6 +484,18 @@ struct rt_context {
   char* ssim_buf = nullptr;  // SSIM kernel weights + per-block partial sums
   size_t ssim_bytes = 0;
   uint64_t primary_pending = 0;  // host-side count of launched primary rays
+  hipStream_t last_stream = nullptr;  // stream of the previous launch (queue-set ordering)
+  bool launched = false;
+  // Tile order (rt_set_tile_order): at scene setup one centre sample per frame
+  // tile is traced (estimate launch); launches then deal their tiles most
+  // expensive first, so the end of a launch is made of cheap tiles.
+  bool order_on = true;
+  unsigned int* est = nullptr;              // device: rays traced per frame tile
+  size_t est_cap = 0;                       // tiles est can hold
+  unsigned long long* est_stats = nullptr;  // the estimate launch's counters (discarded)
+  std::vector<uint32_t> tile_cost;          // host copy (empty: no order)
+  double order_ms = 0;                      // the estimate's wall time at scene setup
+  std::map<std::array<int, 5>, unsigned int*> orders;  // device tile order per launch shape
   // scene specialisation (rt_set_specialize)
   bool specialize = false;
   int accel = RT_ACCEL_BVH | RT_ACCEL_CULL;  // rt_set_accel
@@ -510,6 +522,13 @@ void free_scene(DevScene& s) {
   (void)hipFree(s.blob);
   (void)hipFree(s.accel);
   s = DevScene();
+}
+
+void clear_orders(rt_context* c) {
+  for (auto& kv : c->orders) (void)hipFree(kv.second);
+  c->orders.clear();
+  c->tile_cost.clear();
+  c->order_ms = 0;
 }
 
 template <typename T>
@@ -997,14 +1016,23 @@ void rt_destroy(rt_context* c) {
   (void)hipFree(c->stats);
   (void)hipFree(c->stack);
   (void)hipFree(c->vm_global);
+  clear_orders(c);
+  (void)hipFree(c->est);
+  (void)hipFree(c->est_stats);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
 }
 
+static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntrows, void* d_rgba, void* stream,
+                  bool est);
+static int estimate_costs(rt_context* c);
+
 int rt_set_scene(rt_context* c, const rt_scene* in) {
   if (!c || !in) return fail(RT_E_INVALID, "rt_set_scene: NULL argument");
   if (in->width <= 1 || in->height <= 1) return fail(RT_E_INVALID, "rt_set_scene: width/height must be > 1");
+  if (in->exp_mode < RT_EXP_AMD64_FMA || in->exp_mode > RT_EXP_PORTABLE)
+    return fail(RT_E_INVALID, "rt_set_scene: unknown exp_mode");
   if (in->num_objects < 0 || in->num_lights < 0 || in->num_materials <= 0)
     return fail(RT_E_INVALID, "rt_set_scene: negative counts or no materials");
   if ((in->num_objects > 0 && !in->objects) || (in->num_lights > 0 && !in->lights) || !in->materials)
@@ -1252,6 +1280,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   }
   lights[9] = s.vw;
   lights[10] = s.vh;
+  lights[11] = (double)in->exp_mode;  // RT_EXP_*: the Exp/Log of a fractional Pow
   for (int l = 0; l < s.nlights; l++) {
     double* L = &lights[GLOB + (size_t)l * LGT];
     if (!ext_lights) {
@@ -1327,6 +1356,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     }
   }
   s.num_programs = nprog;
+  if (nprog > 0) s.branching = true;  // a surface program may return a reflective, transparent material
   // per-kind prefix counts (shadow-test counters)
   std::vector<uint32_t> prefb((size_t)(s.nobj + 1) * PREF, 0u);
   for (int i = 0; i < s.nobj; i++) {
@@ -1438,12 +1468,53 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
   free_scene(c->sc);
   c->sc = s;
   c->has_scene = true;
-  return spec_prepare(c);
+  clear_orders(c);
+  int rc = spec_prepare(c);
+  if (rc != RT_OK) return rc;
+  return estimate_costs(c);
+}
+
+// Tile order for a launch of `tiles_x` x `tiles_y` tiles (rows [y0, y1), or
+// tile rows trow0 + j*stride): its tiles by descending estimated cost (the
+// frame tile holding each one's centre), ties in tile order. Cached per launch
+// shape; nullptr without an estimate.
+static int order_for(rt_context* c, int y0, int trow0, int stride, int tiles_x, int tiles_y, const unsigned int** out) {
+  *out = nullptr;
+  if (c->tile_cost.empty()) return RT_OK;
+  const std::array<int, 5> key = {y0, trow0, stride, tiles_x, tiles_y};
+  auto it = c->orders.find(key);
+  if (it != c->orders.end()) {
+    *out = it->second;
+    return RT_OK;
+  }
+  const DevScene& s = c->sc;
+  const int ftx = (s.width + TILE - 1) / TILE, fty = (s.height + TILE - 1) / TILE;
+  const int n = tiles_x * tiles_y;
+  std::vector<uint32_t> cost(n), ord(n);
+  for (int v = 0; v < n; v++) {
+    const int tr = v / tiles_x, tc = v % tiles_x;
+    int fr = stride > 0 ? trow0 + tr * stride : (y0 + tr * TILE + TILE / 2) / TILE;
+    fr = std::min(fr, fty - 1);
+    cost[v] = tc < ftx ? c->tile_cost[(size_t)fr * ftx + tc] : 0u;
+    ord[v] = (uint32_t)v;
+  }
+  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+  unsigned int* d = nullptr;
+  HIP_TRY(hipMalloc((void**)&d, (size_t)n * sizeof(unsigned int)));
+  if (hipMemcpy(d, ord.data(), (size_t)n * sizeof(unsigned int), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return fail(RT_E_DEVICE, "tile order upload failed");
+  }
+  c->orders[key] = d;
+  *out = d;
+  return RT_OK;
 }
 
 // Shared launch: contiguous rows [y0, y1) (stride == 0) or `ntrows` 8-row tile
 // rows starting at tile row trow0 with stride `stride` (y0 = 0, y1 = height).
-static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntrows, void* d_rgba, void* stream) {
+// est: the scene-setup cost estimate (estimate_costs) instead of a render.
+static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntrows, void* d_rgba, void* stream,
+                  bool est) {
   const DevScene& s = c->sc;
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
@@ -1453,10 +1524,11 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int vm_off = lds ? s.blob_bytes : 0;
   const int stack_off = vm_off + ((lds && s.num_programs) ? WG * MAT * (int)sizeof(double) : 0);
   const int cnt_off = stack_off + (s.use_bvh ? WAVES_PER_WG * BVH_STACK * 12 : 0);
-  const int qmask_off = cnt_off + NCNT * WG * (int)sizeof(unsigned long long);
+  const int qmask_off = cnt_off + CNT_BYTES;
   // per-wave object-record stream buffers (global linear scenes, RT_STREAM)
   const int jump_off = qmask_off + 16;  // after the drained-head mask: the sample-0 jump rows
-  const int stream_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);
+  const int board_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);  // work-sharing board (RT_SHARE)
+  const int stream_off = board_off + (RT_SHARE ? BOARD_BYTES : 0);
   // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
   // loads instead: no stream buffers)
   // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)
@@ -1465,7 +1537,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
-  const bool quads = use_quads(c->sched, s, launch_pixels, c->cus);
+  const bool quads = !est && use_quads(c->sched, s, launch_pixels, c->cus);
   const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
   hipFunction_t spec = nullptr;  // built for this scene's flavour (spec_key), this schedule
   {
@@ -1528,6 +1600,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.lds_ext_off = ext_off;
   P.qmask_off = qmask_off;
   P.jump_off = jump_off;
+  P.board_off = board_off;
   P.off_geo = s.off_geo;
   P.off_shade = s.off_shade;
   P.off_mats = s.off_mats;
@@ -1547,7 +1620,8 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // one (launches on a context are stream-ordered): no memset per launch
   P.queue = c->queue + c->qset * QSET;
   P.queue_next = c->queue + (1 - c->qset) * QSET;
-  P.stats = c->stats;
+  P.stats = est ? c->est_stats : c->stats;
+  P.est_out = est ? c->est : nullptr;
 #ifdef RT_PHASE_TIMING
   if (!c->wdiag && hipMalloc((void**)&c->wdiag, sizeof(unsigned long long) * 4 * 8192) != hipSuccess) c->wdiag = nullptr;
   if (c->wdiag) HIP_TRY(hipMemsetAsync(c->wdiag, 0, sizeof(unsigned long long) * 4 * 8192, st));
@@ -1566,7 +1640,13 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.trow_stride = stride;
   P.tiles_x = (s.width + TILE - 1) / TILE;
   int tiles_y = stride > 0 ? ntrows : (y1 - y0 + TILE - 1) / TILE;
-  size_t slots = (size_t)P.tiles_x * tiles_y * TILE * TILE;
+  // estimate: one unit per frame tile; a render: the launch's pixels, its
+  // tiles dealt in order of estimated cost
+  size_t slots = est ? (size_t)P.tiles_x * tiles_y : (size_t)P.tiles_x * tiles_y * TILE * TILE;
+  if (!est) {
+    int rc = order_for(c, y0, trow0, stride, P.tiles_x, tiles_y, &P.order);
+    if (rc != RT_OK) return rc;
+  }
   if (slots >= 0xFFFFFFFFull - 2u * CHUNK * (size_t)grid * WAVES_PER_WG)
     return fail(RT_E_INVALID, "image too large for one launch");
   P.total_slots = (unsigned int)slots;
@@ -1583,7 +1663,13 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     P.bvh_stack_off = stack_off;
   }
 
-  HIP_TRY(hipEventRecord(c->ev0, st));
+  // Launches on a context alternate between two sets of queue heads, each
+  // launch zeroing the other set: a launch on another stream than the
+  // previous one first waits for that launch to end.
+  if (c->launched && st != c->last_stream) HIP_TRY(hipStreamWaitEvent(st, c->ev1, 0));
+  c->last_stream = st;
+  c->launched = true;
+  if (!est) HIP_TRY(hipEventRecord(c->ev0, st));
   const char* blob = s.blob;
   void* args[] = {(void*)&blob, (void*)&P};
   if (spec)
@@ -1593,6 +1679,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   HIP_TRY(hipGetLastError());
   c->qset ^= 1;
   HIP_TRY(hipEventRecord(c->ev1, st));
+  if (est) return RT_OK;
   c->timed = true;
   uint64_t rows = 0;
   if (stride > 0) {
@@ -1607,18 +1694,78 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   return RT_OK;
 }
 
+// Which scenes get a tile order: the estimate traces one sample per 8x8 tile
+// (1/256 of the frame's samples) -- cheap for scenes in LDS or with a BVH, not
+// for the brute-force search over a large scene. RT_TILE_ORDER=0 (environment,
+// experiments) turns it off.
+static bool want_order(const rt_context* c) {
+  static const int env = getenv("RT_TILE_ORDER") ? atoi(getenv("RT_TILE_ORDER")) : 1;
+  const DevScene& s = c->sc;
+  return env != 0 && c->order_on && s.nobj > 0 && (scene_in_lds(s) || s.use_bvh);
+}
+
+// Scene setup: the estimate launch (one centre sample per frame tile, traced
+// rays counted per tile), synchronous, its wall time kept in order_ms.
+static int estimate_costs(rt_context* c) {
+  clear_orders(c);
+  if (!want_order(c)) return RT_OK;
+  const DevScene& s = c->sc;
+  DeviceGuard guard(c->device);
+  const size_t n = (size_t)((s.width + TILE - 1) / TILE) * ((s.height + TILE - 1) / TILE);
+  if (n > c->est_cap) {
+    (void)hipFree(c->est);
+    c->est = nullptr;
+    c->est_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c->est, n * sizeof(unsigned int)));
+    c->est_cap = n;
+  }
+  if (!c->est_stats) HIP_TRY(hipMalloc((void**)&c->est_stats, sizeof(unsigned long long) * 64));
+  const auto t0 = std::chrono::steady_clock::now();
+  HIP_TRY(hipMemset(c->est, 0, n * sizeof(unsigned int)));
+  int rc = launch(c, 0, s.height, 0, 0, 0, nullptr, nullptr, true);
+  if (rc != RT_OK) return rc;
+  std::vector<uint32_t> cost(n);
+  HIP_TRY(hipMemcpy(cost.data(), c->est, n * sizeof(unsigned int), hipMemcpyDeviceToHost));  // (synchronises)
+  unsigned long long wd = 0;
+  HIP_TRY(hipMemcpy(&wd, c->est_stats + ST_WATCHDOG, sizeof wd, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(c->est_stats, 0, sizeof(unsigned long long) * 64));
+  if (wd) return fail(RT_E_DEVICE, "render watchdog in the tile-cost estimate (kernel bug)");
+  c->tile_cost.swap(cost);
+  c->order_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->timed = false;
+  return RT_OK;
+}
+
+int rt_set_tile_order(rt_context* c, int enable) {
+  if (!c) return fail(RT_E_INVALID, "rt_set_tile_order: NULL context");
+  c->order_on = enable != 0;
+  if (!c->has_scene) return RT_OK;
+  if (!c->order_on) {
+    clear_orders(c);
+    return RT_OK;
+  }
+  return c->tile_cost.empty() ? estimate_costs(c) : RT_OK;
+}
+
+int rt_tile_order_info(rt_context* c, int* active, double* estimate_ms) {
+  if (!c || !active || !estimate_ms) return fail(RT_E_INVALID, "rt_tile_order_info: NULL argument");
+  *active = c->tile_cost.empty() ? 0 : 1;
+  *estimate_ms = c->order_ms;
+  return RT_OK;
+}
+
 int rt_render_rows_async(rt_context* c, int y0, int y1, void* d_rgba, void* stream) {
   if (!c || !c->has_scene) return fail(RT_E_INVALID, "rt_render_rows_async: no scene set");
   if (!d_rgba) return fail(RT_E_INVALID, "rt_render_rows_async: NULL output");
   if (y0 < 0 || y1 > c->sc.height || y1 <= y0) return fail(RT_E_INVALID, "rt_render_rows_async: bad row range");
-  return launch(c, y0, y1, 0, 0, 0, d_rgba, stream);
+  return launch(c, y0, y1, 0, 0, 0, d_rgba, stream, false);
 }
 
 int rt_render_tile_rows_async(rt_context* c, int trow0, int trow_stride, int ntrows, void* d_rgba, void* stream) {
   if (!c || !c->has_scene) return fail(RT_E_INVALID, "rt_render_tile_rows_async: no scene set");
   if (!d_rgba) return fail(RT_E_INVALID, "rt_render_tile_rows_async: NULL output");
   if (trow0 < 0 || trow_stride <= 0 || ntrows <= 0) return fail(RT_E_INVALID, "rt_render_tile_rows_async: bad tile rows");
-  return launch(c, 0, c->sc.height, trow0, trow_stride, ntrows, d_rgba, stream);
+  return launch(c, 0, c->sc.height, trow0, trow_stride, ntrows, d_rgba, stream, false);
 }
 
 
@@ -1631,7 +1778,12 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
   HIP_TRY(hipMemcpyAsync(&wd, c->stats + ST_WATCHDOG, sizeof wd, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (wd) {
-    if (reset) (void)hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st);
+    // the frames since the last reset are incomplete: clear everything (as a
+    // reset would) so that later reads report later launches, then fail
+    HIP_TRY(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    c->primary_pending = 0;
+    c->launches = 0;
     return fail(RT_E_DEVICE, "render watchdog: " + std::to_string(wd) + " waves stopped unfinished (kernel bug)");
   }
   std::memset(out, 0, sizeof *out);

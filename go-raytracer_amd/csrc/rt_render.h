@@ -109,7 +109,8 @@ __device__ constexpr bool spec_feat(int f) { return (SPEC_FEAT & f) != 0; }
 // ---------------------------------------------------------------------------
 enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
 // GLOB record (head of the lights section): 0..2 ambient, 3..5 bg start,
-// 6..8 bg end, 9 viewport width, 10 viewport height (read where used, so they
+// 6..8 bg end, 9 viewport width, 10 viewport height, 11 exp mode (RT_EXP_*,
+// the Exp/Log of a fractional Pow) (read where used, so they
 // do not occupy scalar registers across the whole kernel)
 // Frame of one traceRay activation that has children (post-order combine).
 // Global layout: 14 fields, lane-interleaved: Lw[3] cfirst[3] pend_o[3]
@@ -183,13 +184,25 @@ struct Params {
   // [nruns][4] = first index, count, kind, 0 (brute-force scalar-load loops)
   const int* runs;
   int nruns;
-  int cnt_off;    // LDS byte offset of the per-lane event counters [NCNT][WG]
+  int cnt_off;    // LDS byte offset of the event counters (CNT_BYTES)
   int kind_mask;  // bit k: the scene has objects of kind k
+  int board_off;  // LDS byte offset of the work-sharing board (RT_SHARE)
+  // Tile order (host: scene-setup cost estimate, most expensive first): the
+  // pool's virtual tile v renders tile order[v] of the launch; nullptr = in order
+  const unsigned int* order;
+  // Cost-estimate launch (est_out != nullptr): one unit per 8x8 tile of the
+  // frame, its centre pixel's sample 0 traced in full; est_out[tile] counts the
+  // rays traced for it. Serial-sample kernel only; nothing is written to out.
+  unsigned int* est_out;
 };
 // Per-lane event counters (u64, LDS, fire-and-forget ds_add), reduced once per
 // workgroup at exit: per-wave 64-bit SGPR counters pushed the kernel into
 // SGPR spilling (C2 +33% time, C3 +7%).
-enum { CNT_TRACED = 0, CNT_SHADED = 1, CNT_SURFERR = 2, CNT_ST0 = 3, NCNT = CNT_ST0 + RT_NUM_KINDS };
+// Unit events (traced rays, shaded hits, surface errors) are counted per wave
+// (lane 0 adds the ballot's popcount); per-kind shadow-test tallies per lane.
+// LDS: [NUNIT][WAVES_PER_WG] then, CNT_KIND_OFF bytes in, [RT_NUM_KINDS][WG].
+enum { CNT_TRACED = 0, CNT_SHADED = 1, CNT_SURFERR = 2, NUNIT = 3, CNT_KIND_OFF = 128,
+       CNT_BYTES = CNT_KIND_OFF + RT_NUM_KINDS * WG * 8 };
 enum { PREF = 8 };  // u32 per prefix-count entry (RT_NUM_KINDS used, 16-B aligned)
 // BVH node: child 0 box (lo xyz, hi xyz), child 1 box, then as int: ref 0,
 // ref 1, smallest object index under child 0, under child 1. A ref is
@@ -1032,8 +1045,103 @@ __device__ __forceinline__ d3 ld3(const double* f, int field) {
 // CORE field c (0..2 Lw, 3 kr, 4 packed) -> global field index.
 __device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ? 12 : 13); }
 
-// Frame flags (packed with the material index).
-enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16 };
+// Frame flags (packed with the material index): packed = material << PK_MAT |
+// board slot << PK_SLOT | flags. FL_FORKED: the pending refraction child was
+// posted to the workgroup's board (slot PK_SLOT) for another lane to trace.
+enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16, FL_FORKED = 32 };
+enum { PK_SLOT = 8, PK_MAT = 16 };
+
+// ---------------------------------------------------------------------------
+// Work sharing at the tail of a launch (RT_SHARE). Once the queue is drained a
+// lane that finished its last pixel is idle, while other lanes of the group
+// still run the longest pixels: 4 samples one after another, each a binary
+// tree of up to 2^depth - 1 rays when a material both reflects and refracts
+// (raytracer.go:512-556). The lanes of a workgroup share a board in LDS:
+//   * an owner lane posts work it has not started -- the next-to-last of its
+//     pixel's unstarted samples, or the pending refraction child of its
+//     shallowest binary frame -- into a free slot of its wave's range;
+//   * an idle lane of any of the group's waves claims a slot, traces that
+//     sample (PCG state jumped to the sample, raytracer.go:632-643) or subtree
+//     (depth offset = the child's level) on its own stack, and delivers the
+//     colour into the slot;
+//   * the owner joins when it reaches that sample / child: it takes the
+//     delivered colour, or reclaims a slot nobody claimed and traces it itself,
+//     or waits (S_WAIT). The combine and the sample sum then run exactly as
+//     without sharing ((((0 + s0) + s1) + s2) + s3, raytracer.go:651; the
+//     per-level clamp, :557-561), so pixels and counters are unchanged.
+// Slot state lives in two 64-bit LDS masks (posted, delivered) changed by
+// atomics; a wave allocates and frees only the slots of its own range.
+// ---------------------------------------------------------------------------
+#ifndef RT_SHARE
+#ifdef RT_COST_MAP
+#define RT_SHARE 0  // the cost-map diagnostic charges a pixel's work to its own lane
+#else
+#define RT_SHARE 1
+#endif
+#endif
+#ifndef RT_SHARE_SPINS
+#define RT_SHARE_SPINS (1 << 16)  // idle rounds (s_sleep'd) a drained wave waits for work before leaving
+#endif
+#ifndef RT_SHARE_SLEEP
+#define RT_SHARE_SLEEP 127  // s_sleep per idle round (x64 cycles): a polling wave keeps the issue slots of
+                            // other workgroups' waves on its SIMD almost free
+#endif
+#ifndef RT_SHARE_SAMPLES
+#define RT_SHARE_SAMPLES 1  // post unstarted samples (serial schedule), not only refraction subtrees
+#endif
+enum { NSLOT = 64, SLOTS_PER_WAVE = NSLOT / WAVES_PER_WG, S_WAIT = 4 };
+struct Board {
+  unsigned long long post;           // slots holding a task nobody has claimed
+  unsigned long long done;           // slots whose colour has been delivered
+  unsigned int wfree[WAVES_PER_WG];  // per wave: free slots of its range (bit j: slot SLOTS_PER_WAVE * w + j)
+  int nidle;                         // idle lanes of drained waves (helpers available)
+  int nactive;                       // waves with busy lanes
+  int pad[2];
+  // subtree task: the pending refraction ray (origin, direction), read by the
+  // helper when it claims the slot; then the delivered colour (res = ray[0..2])
+  double ray[NSLOT][6];
+  int meta[NSLOT][2];  // subtree: depth offset, 0; sample: x | k << 16 | 1 << 30, y
+};
+enum { BOARD_BYTES = (int)sizeof(Board), META_SAMPLE = 1 << 30 };
+#define RT_WG_SCOPE __HIP_MEMORY_SCOPE_WORKGROUP
+__device__ __forceinline__ bool board_reclaim(Board* b, int q) {  // owner: take back a task nobody claimed
+  const unsigned long long old = __hip_atomic_fetch_and(&b->post, ~(1ull << q), __ATOMIC_ACQUIRE, RT_WG_SCOPE);
+  return ((old >> q) & 1ull) != 0;
+}
+__device__ __forceinline__ bool board_done(Board* b, int q) {
+  return ((__hip_atomic_load(&b->done, __ATOMIC_ACQUIRE, RT_WG_SCOPE) >> q) & 1ull) != 0;
+}
+__device__ __forceinline__ void board_free(Board* b, int q) {
+  __hip_atomic_fetch_or(&b->wfree[q / SLOTS_PER_WAVE], 1u << (q % SLOTS_PER_WAVE), __ATOMIC_RELAXED, RT_WG_SCOPE);
+}
+// owner: the delivered colour of slot q (after board_done), slot freed
+__device__ __forceinline__ d3 board_take(Board* b, int q) {
+  const d3 r = mk(b->ray[q][0], b->ray[q][1], b->ray[q][2]);
+  __hip_atomic_fetch_and(&b->done, ~(1ull << q), __ATOMIC_RELAXED, RT_WG_SCOPE);
+  board_free(b, q);
+  return r;
+}
+__device__ __forceinline__ void board_deliver(Board* b, int q, d3 c) {  // helper
+  b->ray[q][0] = c.x;
+  b->ray[q][1] = c.y;
+  b->ray[q][2] = c.z;
+  __hip_atomic_fetch_or(&b->done, 1ull << q, __ATOMIC_RELEASE, RT_WG_SCOPE);
+}
+// Position of the r-th set bit of m (r < popcount(m)).
+__device__ __forceinline__ int nth_bit(uint64_t m, int r) {
+  for (int i = 0; i < r; i++) m &= m - 1;
+  return __builtin_ctzll(m);
+}
+// The lowest n set bits of m.
+__device__ __forceinline__ uint64_t low_bits(uint64_t m, int n) {
+  uint64_t r = 0;
+  for (int i = 0; i < n && m; i++) {
+    const uint64_t b = m & (~m + 1);
+    r |= b;
+    m ^= b;
+  }
+  return r;
+}
 
 
 // ---------------------------------------------------------------------------
@@ -1198,6 +1306,18 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // drained-head mask of this workgroup
   unsigned int* qdrained = reinterpret_cast<unsigned int*>(smem + P.qmask_off);
   if (threadIdx.x == 0) *qdrained = 0u;
+  // per-wave unit counters: zeroed before the barrier (any wave's lane 0 adds)
+  if (threadIdx.x < NUNIT * WAVES_PER_WG) reinterpret_cast<unsigned long long*>(smem + P.cnt_off)[threadIdx.x] = 0ull;
+  Board* Bd = reinterpret_cast<Board*>(smem + P.board_off);
+  if constexpr (RT_SHARE) {
+    if (threadIdx.x == 0) {
+      Bd->post = 0ull;
+      Bd->done = 0ull;
+      Bd->nidle = 0;
+      Bd->nactive = 0;
+    }
+    if (threadIdx.x < WAVES_PER_WG) Bd->wfree[threadIdx.x] = (1u << SLOTS_PER_WAVE) - 1u;
+  }
   if (blockIdx.x == 0 && threadIdx.x < QHEADS) atomicExch(P.queue_next + threadIdx.x * QSTRIDE, 0u);
   if constexpr (LDS) {
     const int n16 = P.blob_bytes / 16;
@@ -1322,6 +1442,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   bool need_gen = false;  // lane waits for its next sample ray
   int px = 0, py = 0, sample = 0, sp = 0;
   unsigned int pout = 0;  // output pixel index
+  // work sharing (RT_SHARE): the lane's own samples are [0, own_end) -- the
+  // rest were posted, sample k to board slot (sfork >> 8k) & 63; pend bit L:
+  // frame L holds a pending refraction child not yet posted; task >= 0: the
+  // lane runs a claimed task for slot `task`, its tree rooted at level dbase
+  int own_end = 4, task = -1, dbase = 0;
+  uint32_t sfork = 0u, pend = 0u;
+  const int wave = (int)(threadIdx.x >> 6);
+  int my_idle = 0, spins = 0;  // wave-uniform: idle lanes this wave reports, idle rounds
+  bool my_active = false;      // wave-uniform: counted in Bd->nactive
+  bool resumed = false;        // a waiting owner's helper delivered (taken by the TRACE pass's unwind)
   int hit_i = 0, hit_f = 0;
   double hit_t = 0.0;
   Pcg rng{0, 0};
@@ -1335,8 +1465,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   int qhead = 0;  // queue heads tried so far (QHEADS)
   bool exhausted = false;
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off);
-  for (int k = 0; k < NCNT; k++) cnt[k * WG + threadIdx.x] = 0;
-  auto cnt_add = [&](int k, uint64_t v) { atomicAdd(&cnt[k * WG + threadIdx.x], (unsigned long long)v); };
+  unsigned long long* kcnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off + CNT_KIND_OFF);
+  for (int k = 0; k < RT_NUM_KINDS; k++) kcnt[k * WG + threadIdx.x] = 0;
+  // shadow tests of kind k (per lane)
+  auto cnt_kind = [&](int k, uint64_t v) { atomicAdd(&kcnt[k * WG + threadIdx.x], (unsigned long long)v); };
+  // a unit event on the lanes where b holds (wave-uniform call)
+  auto cnt_unit = [&](int k, bool b) {
+    const unsigned int n = (unsigned int)__popcll(__ballot(b));
+    if (lane == 0 && n) atomicAdd(&cnt[k * WAVES_PER_WG + wave], (unsigned long long)n);
+  };
   WaveStack bst;
   bst.mask = reinterpret_cast<uint64_t*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
   bst.ref = reinterpret_cast<int*>(smem + P.bvh_stack_off + WAVES_PER_WG * BVH_STACK * 8) + (threadIdx.x >> 6) * BVH_STACK;
@@ -1361,36 +1498,85 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     ray.d = norm(sub(ray.o, eye));
   };
 
+  // PCG state at the start of sample k of pixel (x, y): the strip seed
+  // (raytracer.go:632-634) jumped 8*(y mod 20) + 2*k draws.
+  auto sample_rng = [&](int x, int y, int k) {
+    const int ry = y % 20;
+    const uint64_t* j = P.jump + (ry * 4 + k) * 4;
+    return pcg_jump(Pcg{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)(y - ry)}, j[0], j[1], j[2], j[3]);
+  };
+  // The board slot a waiting owner (S_WAIT) waits on: its posted sample
+  // `sample` (at sp == 0), else the posted refraction child of frame sp - 1.
+  auto wait_slot = [&]() -> int {
+    if (!QD && sp == 0) return (int)((sfork >> (8 * sample)) & 63u);
+    return (int)((__double_as_longlong(core_ld(sp - 1, 4)) >> PK_SLOT) & 63);
+  };
+  // Serial samples: account sample `sample` onwards after the lane finished
+  // the one before -- run it (own), take a helper's colour, reclaim a posted
+  // sample nobody claimed, or wait; quantise once all 4 are summed.
+  auto advance_sample = [&]() {
+    for (;;) {
+      if (P.est_out && sample == 1) {  // cost estimate: one sample per tile
+        state = S_IDLE;
+        return;
+      }
+      if (sample == 4) {
+        d3 c = scale(sum, 1.0 / 4.0);  // raytracer.go:656 -> vec.go:104-107
+        uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
+        uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
+        uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
+#ifdef RT_COST_MAP
+        P.out[pout] = lane_cost;
+        lane_cost = 0;
+#else
+        P.out[pout] = (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+#endif
+        state = S_IDLE;
+        return;
+      }
+      if (!RT_SHARE || sample < own_end) {
+        need_gen = true;  // next sample ray, generated in one uniform block
+        state = S_TRACE;
+        return;
+      }
+      const int q = (int)((sfork >> (8 * sample)) & 63u);
+      if (board_reclaim(Bd, q)) {  // nobody took it: trace it here
+        board_free(Bd, q);
+        own_end = sample + 1;
+        rng = sample_rng(px, py, sample);
+        need_gen = true;
+        state = S_TRACE;
+        return;
+      }
+      if (!board_done(Bd, q)) {
+        state = S_WAIT;  // (the slot is found again from sfork: wait_slot)
+        return;
+      }
+      sum = add(sum, board_take(Bd, q));  // raytracer.go:651, in sample order
+      sample++;
+    }
+  };
+
   // Propagate a finished traceRay colour up the lane's frame stack
   // (post-order, raytracer.go:528/554/557-561); ends with the lane either
-  // tracing its next ray (pending refraction child / next sample) or idle.
+  // tracing its next ray (pending refraction child / next sample), waiting
+  // for a helper (S_WAIT) or idle.
   auto unwind = [&](bool have_res, d3 res, bool pf_valid, long long pf_packed, d3 pf_lw, double pf_kr) {
     while (__any(have_res)) {
       if (have_res) {
         if (sp == 0) {
-          if constexpr (QD) {
+          if (RT_SHARE && task >= 0) {  // a claimed task: hand the colour to its owner
+            board_deliver(Bd, task, res);
+            task = -1;
+            dbase = 0;
+            state = S_IDLE;
+          } else if constexpr (QD) {
             sum = res;  // this sample's colour, summed by the quad's first lane (main loop)
             state = S_DONE;
           } else {
-          sum = add(sum, res);  // raytracer.go:651
-          sample++;
-          if (sample == 4) {
-            d3 c = scale(sum, 1.0 / 4.0);  // raytracer.go:656 -> vec.go:104-107
-            uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
-            uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
-            uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
-#ifdef RT_COST_MAP
-            P.out[pout] = lane_cost;
-            lane_cost = 0;
-#else
-            P.out[pout] =
-                (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
-#endif
-            state = S_IDLE;
-          } else {
-            need_gen = true;  // next sample ray, generated in one uniform block
-            state = S_TRACE;
-          }
+            sum = add(sum, res);  // raytracer.go:651
+            sample++;
+            advance_sample();
           }
           have_res = false;
         } else {
@@ -1405,12 +1591,29 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             // reflection child done; trace the pending refraction child
             st3(ext(sp - 1), 0, res);
             core_st(sp - 1, 4, __longlong_as_double(packed | FL_STAGE));
-            ray.o = ld3(ext(sp - 1), 3);
-            ray.d = ld3(ext(sp - 1), 6);
-            state = S_TRACE;
-            have_res = false;
+            if (RT_SHARE) pend &= ~(1u << (sp - 1));
+            if (RT_SHARE && (fl & FL_FORKED)) {
+              const int q = (int)((packed >> PK_SLOT) & 63);
+              if (board_reclaim(Bd, q)) {  // nobody took it: trace it here
+                board_free(Bd, q);
+                ray.o = ld3(ext(sp - 1), 3);
+                ray.d = ld3(ext(sp - 1), 6);
+                state = S_TRACE;
+                have_res = false;
+              } else if (board_done(Bd, q)) {
+                res = board_take(Bd, q);  // the next round combines (FL_STAGE set)
+              } else {
+                state = S_WAIT;  // (the slot is found again from the frame: wait_slot)
+                have_res = false;
+              }
+            } else {
+              ray.o = ld3(ext(sp - 1), 3);
+              ray.d = ld3(ext(sp - 1), 6);
+              state = S_TRACE;
+              have_res = false;
+            }
           } else {
-            const double* FM = S.mats + (size_t)(packed >> 8) * MAT;
+            const double* FM = S.mats + (size_t)(packed >> PK_MAT) * MAT;
             d3 R = mk(0, 0, 0), Tr = mk(0, 0, 0);
             if ((fl & FL_HASR) && (fl & FL_HAST)) {
               R = ld3(ext(sp - 1), 0);
@@ -1526,8 +1729,29 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                                    : __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
       unsigned int take = min((unsigned int)__popcll(mask), pool_end - pool_next);
+      if (!QD && P.est_out) {  // cost estimate: unit u = the centre pixel of frame tile u
+        if (need && rank < take) {
+          const unsigned int u = pool_next + rank;
+          px = min((int)(u % (unsigned)P.tiles_x) * TILE + TILE / 2, P.width - 1);
+          py = min((int)(u / (unsigned)P.tiles_x) * TILE + TILE / 2, P.y1 - 1);
+          pout = u;
+          const int ry = py % 20;
+          rng = pcg_jump(Pcg{0xDEADULL ^ (uint64_t)px, 0xBEEFULL ^ (uint64_t)(py - ry)}, jrows[ry * 4],
+                         jrows[ry * 4 + 1], jrows[ry * 4 + 2], jrows[ry * 4 + 3]);
+          sample = 0;
+          own_end = 1;
+          sum = mk(0, 0, 0);
+          sp = 0;
+          pend = 0u;
+          need_gen = true;
+          state = S_TRACE;
+        }
+        pool_next += take;
+        continue;
+      }
       // a pool never crosses a tile: the tile's position is wave-uniform
-      const unsigned int tile = pool_next / (TILE * TILE);
+      unsigned int tile = pool_next / (TILE * TILE);
+      if (P.order) tile = P.order[tile];
       const int trow = (int)(tile / (unsigned)P.tiles_x);
       const int x0 = (int)((tile % (unsigned)P.tiles_x) * TILE);
       const int orow0 = trow * TILE;
@@ -1555,13 +1779,145 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sum = mk(0, 0, 0);
           sp = 0;
+          own_end = 4;
+          pend = 0u;
           need_gen = true;
           state = S_TRACE;
         }
       }
       pool_next += take;
     }
-    if (!__any(state != S_IDLE)) break;
+    if constexpr (RT_SHARE) {
+      // ---- work sharing within the workgroup (see Board) ----
+      // (a) owners whose helper delivered take the colour; it is propagated
+      // by the TRACE pass's unwind (a posted sample is added in sample order
+      // at sp == 0, a posted refraction child combined at its frame)
+      if (__any(state == S_WAIT)) {
+        resumed = state == S_WAIT && board_done(Bd, wait_slot());
+      }
+      // (b) owners post work they have not started, while drained waves of
+      // the group have idle lanes to take it
+      const int nid = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&Bd->nidle, __ATOMIC_RELAXED, RT_WG_SCOPE));
+      if (nid > 0) {
+        const uint64_t pm = __hip_atomic_load(&Bd->post, __ATOMIC_RELAXED, RT_WG_SCOPE);
+        const int want = nid - (int)__popcll(((uint64_t)__builtin_amdgcn_readfirstlane((int)(pm >> 32)) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readfirstlane((int)pm));
+        const bool busy_lane = state == S_TRACE || state == S_SHADE || state == S_WAIT;
+        const bool cs = !QD && RT_SHARE_SAMPLES && busy_lane && task < 0 && own_end - 1 > sample;  // an unstarted own sample
+        const bool cand = cs || (busy_lane && pend != 0u);
+        const uint64_t cm = __ballot(cand);
+        if (want > 0 && cm) {
+          const uint32_t wf = (uint32_t)__builtin_amdgcn_readfirstlane(
+              (int)__hip_atomic_load(&Bd->wfree[wave], __ATOMIC_RELAXED, RT_WG_SCOPE));
+          const int npost = min(min((int)__popcll(cm), (int)__popc(wf)), want);
+          if (npost > 0) {
+            const uint32_t used = (uint32_t)low_bits(wf, npost);
+            const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned int)(cm >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((unsigned int)cm, 0u));
+            if (cand && rk < npost) {
+              const int q = wave * SLOTS_PER_WAVE + nth_bit(wf, rk);
+              if (cs) {  // the last of the lane's unstarted samples
+                const int k = own_end - 1;
+                Bd->meta[q][0] = px | (k << 16) | META_SAMPLE;
+                Bd->meta[q][1] = py;
+                own_end = k;
+                sfork = (sfork & ~(0xffu << (8 * k))) | ((uint32_t)q << (8 * k));
+              } else {  // the pending refraction child of the shallowest binary frame
+                const int L = __builtin_ctz(pend);
+                const double* e = ext(L);
+                const d3 o = ld3(e, 3), dd = ld3(e, 6);
+                Bd->ray[q][0] = o.x;
+                Bd->ray[q][1] = o.y;
+                Bd->ray[q][2] = o.z;
+                Bd->ray[q][3] = dd.x;
+                Bd->ray[q][4] = dd.y;
+                Bd->ray[q][5] = dd.z;
+                Bd->meta[q][0] = dbase + L + 1;
+                Bd->meta[q][1] = 0;
+                const long long pk = __double_as_longlong(core_ld(L, 4));
+                core_st(L, 4, __longlong_as_double(pk | FL_FORKED | ((long long)q << PK_SLOT)));
+                pend &= ~(1u << L);
+              }
+            }
+            if (lane == 0) {
+              __hip_atomic_fetch_and(&Bd->wfree[wave], ~used, __ATOMIC_RELAXED, RT_WG_SCOPE);
+              __hip_atomic_fetch_or(&Bd->post, (uint64_t)used << (wave * SLOTS_PER_WAVE), __ATOMIC_RELEASE,
+                                    RT_WG_SCOPE);
+            }
+          }
+        }
+      }
+      // (c) idle lanes of a drained wave claim posted tasks
+      uint64_t il = exhausted ? __ballot(state == S_IDLE) : 0ull;
+      if (il) {
+        const uint64_t pm0 = __hip_atomic_load(&Bd->post, __ATOMIC_RELAXED, RT_WG_SCOPE);
+        const uint64_t pm = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(pm0 >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)pm0);
+        if (pm) {
+          const uint64_t want = low_bits(pm, (int)__popcll(il));
+          uint64_t old = 0;
+          if (lane == 0) old = __hip_atomic_fetch_and(&Bd->post, ~want, __ATOMIC_ACQUIRE, RT_WG_SCOPE);
+          const uint64_t got = want & (((uint64_t)__builtin_amdgcn_readfirstlane((int)(old >> 32)) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)old));
+          const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned int)(il >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned int)il, 0u));
+          if (state == S_IDLE && rk < (int)__popcll(got)) {
+            const int q = nth_bit(got, rk);
+            const int m0 = Bd->meta[q][0];
+            if (m0 & META_SAMPLE) {  // sample k of pixel (x, y)
+              px = m0 & 0xffff;
+              py = Bd->meta[q][1];
+              sample = (m0 >> 16) & 3;
+              own_end = sample + 1;
+              rng = sample_rng(px, py, sample);
+              need_gen = true;
+              dbase = 0;
+            } else {  // a refraction subtree rooted at level m0
+              ray.o = mk(Bd->ray[q][0], Bd->ray[q][1], Bd->ray[q][2]);
+              ray.d = mk(Bd->ray[q][3], Bd->ray[q][4], Bd->ray[q][5]);
+              dbase = m0;
+            }
+            task = q;
+            sp = 0;
+            pend = 0u;
+            state = S_TRACE;
+          }
+          il = __ballot(state == S_IDLE);
+        }
+      }
+      // (d) bookkeeping for the board: helpers available, waves still busy
+      const int cur_idle = P.est_out ? 0 : (int)__popcll(il);
+      if (cur_idle != my_idle) {
+        if (lane == 0) __hip_atomic_fetch_add(&Bd->nidle, cur_idle - my_idle, __ATOMIC_RELAXED, RT_WG_SCOPE);
+        my_idle = cur_idle;
+      }
+      const bool busy = __any(state != S_IDLE);
+      if (busy != my_active) {
+        if (lane == 0) __hip_atomic_fetch_add(&Bd->nactive, busy ? 1 : -1, __ATOMIC_RELAXED, RT_WG_SCOPE);
+        my_active = busy;
+      }
+      if (!busy) {
+        // drained (the refill found nothing): wait while the group may still
+        // post work; leave once no wave is busy and nothing is posted
+        const int na = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&Bd->nactive, __ATOMIC_RELAXED, RT_WG_SCOPE));
+        const uint64_t pm = __hip_atomic_load(&Bd->post, __ATOMIC_RELAXED, RT_WG_SCOPE);
+        if ((na == 0 && __builtin_amdgcn_readfirstlane((int)(pm >> 32)) == 0 &&
+             __builtin_amdgcn_readfirstlane((int)pm) == 0) ||
+            ++spins > RT_SHARE_SPINS) {
+          if (lane == 0 && my_idle) __hip_atomic_fetch_add(&Bd->nidle, -my_idle, __ATOMIC_RELAXED, RT_WG_SCOPE);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(RT_SHARE_SLEEP);
+        continue;
+      }
+      spins = 0;
+      if (!__any(state == S_TRACE || state == S_SHADE || resumed)) {  // only waiting (or quad-holding) lanes
+        __builtin_amdgcn_s_sleep(RT_SHARE_SLEEP / 4);
+        continue;
+      }
+    } else {
+      if (!__any(state != S_IDLE)) break;
+    }
     // ---- new sample rays for every lane that needs one, in one block ----
     if (__any(need_gen)) {
       if (need_gen) {
@@ -1572,7 +1928,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     PH_MARK(0);
 
     // ---- TRACE pass: closestHit over all objects (raytracer.go:469-483) ----
-    if (__any(state == S_TRACE)) {
+    if (__any(state == S_TRACE || resumed)) {
       const bool tr = state == S_TRACE;
       // Prefetch the parent frame: a ray that misses pops it right after
       // this pass, and the load latency hides under the object loop.
@@ -1728,7 +2084,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           }
         }
       }
-      if (tr) cnt_add(CNT_TRACED, 1);
+      cnt_unit(CNT_TRACED, tr);
+      if (!QD && P.est_out && tr) atomicAdd(P.est_out + pout, 1u);
       PH_MARK(1);
       d3 res = mk(0, 0, 0);
       if (tr) {
@@ -1742,7 +2099,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           res = lerp(mk(G[3], G[4], G[5]), mk(G[6], G[7], G[8]), t);
         }
       }
-      unwind(tr && !found, res, pf, pf_packed, pf_lw, pf_kr);
+      if (RT_SHARE && resumed) res = board_take(Bd, wait_slot());  // (not tracing: pf is false)
+      unwind((tr && !found) || (RT_SHARE && resumed), res, pf, pf_packed, pf_lw, pf_kr);
+      resumed = false;
       PH_MARK(2);
     }
 
@@ -1752,7 +2111,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (nsh == 0 || (ntr != 0 && nsh * RT_SHADE_DEN < (nsh + ntr) * RT_SHADE_NUM)) continue;
 
     const bool hit = state == S_SHADE;
-    if (hit) cnt_add(CNT_SHADED, 1);
+    cnt_unit(CNT_SHADED, hit);
     // ComputeSurfaceProps (raytracer.go:106-122, 182-194, 242-260, 339-370)
     d3 pw = mk(0, 0, 0), nw = mk(0, 0, 1);
     int mat = 0;
@@ -1829,7 +2188,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         surf_bad = bad;
       }
     }
-    if (surf_bad) cnt_add(CNT_SURFERR, 1);
+    cnt_unit(CNT_SURFERR, surf_bad);
 
     // computeLighting + inShadow (raytracer.go:372-429)
     PH_MARK(3);
@@ -2229,8 +2588,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         sc1 += pe.y - (hk == 1 ? 1u : 0u);
         sc2 += pe.z - (hk == 2 ? 1u : 0u);
         sc3 += pe.w - (hk == 3 ? 1u : 0u);
-        if (spec_kind(4) && (P.kind_mask & 16)) cnt_add(CNT_ST0 + 4, pe4 - (hk == 4 ? 1u : 0u));  // cones, CSG: rare, flushed per light
-        if (spec_kind(5) && (P.kind_mask & 32)) cnt_add(CNT_ST0 + 5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
+        if (spec_kind(4) && (P.kind_mask & 16)) cnt_kind(4, pe4 - (hk == 4 ? 1u : 0u));  // cones, CSG: rare, flushed per light
+        if (spec_kind(5) && (P.kind_mask & 32)) cnt_kind(5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
       }
       PH_MARK(4);
 #if defined(RT_SPEC_NLIGHTS) && RT_LIGHT_SPLIT
@@ -2257,10 +2616,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         d3 lcol = mk(lt[3], lt[4], lt[5]);
         if (spec_feat(SF_LSPOT) && (int)lt[9] == RT_LIGHT_SPOT) {  // extension: cone falloff
           const double ca = dot(neg(ldir_a[li]), mk(lt[6], lt[7], lt[8]));
-          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11]) : 0.0);
+          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11], (int)G[11]) : 0.0);
         }
         d3 diffuse = scale(lcol, ndl_a[li] * M[9]);
-        const double pw_s = pok_a[li] ? pow_a[li] : go_pow(spec_a[li], M[11]);
+        const double pw_s = pok_a[li] ? pow_a[li] : go_pow(spec_a[li], M[11], (int)G[11]);
         d3 specular = scale(lcol, M[10] * pw_s);
         L = add(add(L, diffuse), specular);
       }
@@ -2271,23 +2630,23 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         d3 lcol = mk(lt[3], lt[4], lt[5]);
         if (spec_feat(SF_LSPOT) && lkind == RT_LIGHT_SPOT) {  // extension: cone falloff
           const double ca = dot(neg(ldir), mk(lt[6], lt[7], lt[8]));
-          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11]) : 0.0);
+          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11], (int)G[11]) : 0.0);
         }
         double ndl = go_max0(dot(nw, ldir));
         d3 diffuse = scale(lcol, ndl * M[9]);
         d3 H = norm(add(neg(ray.d), ldir));
         double spec = go_max0(dot(nw, H));
-        d3 specular = scale(lcol, M[10] * go_pow(spec, M[11]));
+        d3 specular = scale(lcol, M[10] * go_pow(spec, M[11], (int)G[11]));
         L = add(add(L, diffuse), specular);
       }
       PH_MARK(5);
     }
 #endif
     if (hit) {
-      if (spec_kind(0) && (P.kind_mask & 1)) cnt_add(CNT_ST0 + 0, sc0);
-      if (spec_kind(1) && (P.kind_mask & 2)) cnt_add(CNT_ST0 + 1, sc1);
-      if (spec_kind(2) && (P.kind_mask & 4)) cnt_add(CNT_ST0 + 2, sc2);
-      if (spec_kind(3) && (P.kind_mask & 8)) cnt_add(CNT_ST0 + 3, sc3);
+      if (spec_kind(0) && (P.kind_mask & 1)) cnt_kind(0, sc0);
+      if (spec_kind(1) && (P.kind_mask & 2)) cnt_kind(1, sc1);
+      if (spec_kind(2) && (P.kind_mask & 4)) cnt_kind(2, sc2);
+      if (spec_kind(3) && (P.kind_mask & 8)) cnt_kind(3, sc3);
     }
 
     // traceRay body after lighting (raytracer.go:505-561)
@@ -2346,8 +2705,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           kr = r0 + (1 - r0) * go_pow(1 - cost, 5);
           lw = scale(L, 1.0 - T);
         }
-        const int d = P.depth - sp;  // depth of the current ray
+        const int d = P.depth - dbase - sp;  // depth of the current ray
         if (d - 1 > 0 && (hasR || hasT)) {
+          if (RT_SHARE && hasR && hasT) pend |= 1u << sp;  // the refraction child waits: may be posted
           core_st(sp, 0, lw.x);
           core_st(sp, 1, lw.y);
           core_st(sp, 2, lw.z);
@@ -2361,7 +2721,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             st3(f, 14, col);
             f[17 * 64] = refl;
           }
-          long long packed = ((long long)(mat < 0 ? 0 : mat) << 8) | (mat < 0 ? FL_VMMAT : 0) |
+          long long packed = ((long long)(mat < 0 ? 0 : mat) << PK_MAT) | (mat < 0 ? FL_VMMAT : 0) |
                              (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
           core_st(sp, 4, __longlong_as_double(packed));
           sp++;
@@ -2401,11 +2761,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // Workgroup reduction of the per-lane counters (every wave of the group
   // leaves the main loop, so all reach the barrier).
   __syncthreads();
-  if (threadIdx.x < NCNT) {
+  if (threadIdx.x < RT_NUM_KINDS) {
     unsigned long long sum = 0;
-    for (int j = 0; j < WG; j++) sum += cnt[threadIdx.x * WG + j];
-    const int k = (int)threadIdx.x;
-    const int slot = k == CNT_TRACED ? ST_TRACED : (k == CNT_SHADED ? ST_SHADED : (k == CNT_SURFERR ? ST_SURFERR : ST_STESTS + (k - CNT_ST0)));
+    for (int j = 0; j < WG; j++) sum += kcnt[threadIdx.x * WG + j];
+    if (sum) atomicAdd(P.stats + ST_STESTS + threadIdx.x, sum);
+  } else if (threadIdx.x < RT_NUM_KINDS + NUNIT) {
+    const int k = (int)threadIdx.x - RT_NUM_KINDS;
+    unsigned long long sum = 0;
+    for (int j = 0; j < WAVES_PER_WG; j++) sum += cnt[k * WAVES_PER_WG + j];
+    const int slot = k == CNT_TRACED ? ST_TRACED : (k == CNT_SHADED ? ST_SHADED : ST_SURFERR);
     if (sum) atomicAdd(P.stats + slot, sum);
     // one inShadow call per (shaded hit, light)
     if (k == CNT_SHADED && sum) atomicAdd(P.stats + ST_SHADOW, sum * (unsigned long long)P.nlights);

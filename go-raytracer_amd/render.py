@@ -71,6 +71,10 @@ def load_library(path=None):
     l.rt_specialized.restype = i
     l.rt_spec_precompile.argtypes = [i, C.POINTER(i), i, C.POINTER(C.c_double)]
     l.rt_spec_precompile.restype = i
+    l.rt_set_tile_order.argtypes = [vp, i]
+    l.rt_set_tile_order.restype = i
+    l.rt_tile_order_info.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
+    l.rt_tile_order_info.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
     l.rt_render.restype = i
     if l.rt_abi_version() != abi.RT_ABI_VERSION:
@@ -143,6 +147,19 @@ class RenderContext:
         RT_SCHED_PIXEL or RT_SCHED_QUADS -- how pixels are dealt to lanes;
         identical pixels and counters. Applies at the next set_scene."""
         _check(self.lib.rt_set_schedule(self.handle, int(mode)), "rt_set_schedule")
+
+    def set_tile_order(self, enable=True):
+        """Deal each launch's tiles most expensive first (default on; the
+        estimate -- one centre sample per 8x8 tile -- runs at scene setup);
+        identical pixels and counters either way. Applies at once."""
+        _check(self.lib.rt_set_tile_order(self.handle, int(bool(enable))), "rt_set_tile_order")
+
+    def tile_order_info(self):
+        """(active, estimate_ms): whether the current scene's launches use a
+        tile order, and the estimate's wall time at scene setup."""
+        a, ms = C.c_int(), C.c_double()
+        _check(self.lib.rt_tile_order_info(self.handle, C.byref(a), C.byref(ms)), "rt_tile_order_info")
+        return bool(a.value), ms.value
 
     def scene_info(self):
         """rt_scene_info flags of the current scene (abi.RT_INFO_*): which

@@ -193,6 +193,10 @@ class RenderArgs:
     # GML EvalState at the render call (per-frame clone, raytracer.go:738-751):
     # closure surfaces evaluate on its stack. None for scenes built in Python.
     state: object = None
+    # Which math.Exp / math.Log a fractional Pow exponent runs (rt_scene.exp_mode,
+    # abi.RT_EXP_*): Go's amd64 assembly with FMA by default (the reference's
+    # deployment on an x86-64 CPU with AVX2+FMA).
+    exp_mode: int = 0
 
 
 _NFACES = {abi.RT_SPHERE: 1, abi.RT_PLANE: 1, abi.RT_CUBE: 6, abi.RT_CYLINDER: 3, abi.RT_CONE: 2}
@@ -418,6 +422,7 @@ def convert(args: RenderArgs) -> abi.PackedScene:
         sc.program_code_words = len(words)
         sc.program_const_count = len(consts)
         packed_progs = (c_code, c_consts, c_entry, [sf for sf, _ in programs], args.state)
+    sc.exp_mode = int(args.exp_mode)
     packed = abi.PackedScene(sc, c_lights, c_objs, c_mats, packed_progs, c_ext)
     packed._csg = (c_leaves, c_code)
     return packed

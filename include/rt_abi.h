@@ -36,7 +36,10 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
+#define RT_EXP_AMD64_FMA 0
+#define RT_EXP_AMD64 1
+#define RT_EXP_PORTABLE 2
 
 /* Status codes. */
 #define RT_OK 0
@@ -166,8 +169,8 @@ typedef struct rt_light {
 #define RT_VM_FLOOR 19 /* i64 of floor(x) (amd64 float64 -> int64 conversion) */
 #define RT_VM_FRAC 20  /* x - float64(int64(x)) */
 #define RT_VM_SQRT 21
-#define RT_VM_SIN 22   /* Go math.Sin(x * Pi/180): GML angles are degrees */
-#define RT_VM_COS 23
+#define RT_VM_SIN 22   /* Go math.Sin(0.017453292519943295 * x), one product (evaluator.go:932 DegToRad): GML angles are degrees */
+#define RT_VM_COS 23   /* Go math.Cos(0.017453292519943295 * x) */
 #define RT_VM_CLAMPF 24 /* f64 clamped to [0, 1] */
 #define RT_VM_CLAMPI 25 /* i64 clamped to [0, 1] */
 #define RT_VM_TBL 26   /* r[d] = consts[c + 1 + clamp(r[a], 0, n - 1)], n = consts[c] (guard with ERR) */
@@ -215,7 +218,13 @@ typedef struct rt_scene {
     int32_t num_programs;
     int32_t program_code_words;
     int32_t program_const_count;
-    int32_t reserved0;
+    /* ABI 3: which math.Exp / math.Log a fractional math.Pow exponent
+     * (raytracer.go:395 specular n, spot exponents) runs -- Go dispatches them
+     * per platform: RT_EXP_AMD64_FMA (0, default) exp_amd64.s with FMA, what
+     * the reference runs on an x86-64 CPU with AVX2+FMA; RT_EXP_AMD64 (1) the
+     * same without FMA; RT_EXP_PORTABLE (2) exp.go / log.go (platforms with
+     * no assembly Exp). Integer exponents never reach Exp. */
+    int32_t exp_mode;
     /* ABI 2: when num_ext_lights > 0 these are the scene's lights, in program
      * order, and lights / num_lights are ignored. */
     const rt_light *ext_lights;
@@ -276,7 +285,9 @@ int rt_set_scene(rt_context *ctx, const rt_scene *scene);
  * = the null stream) into device memory `d_rgba` (row y0 first, stride
  * 4*width bytes). Asynchronous; device pointers only. The per-row pixels are
  * identical to rows y0..y1-1 of a full-frame Render(): RNG state depends only
- * on (x, 20-row strip) (raytracer.go:627-634). */
+ * on (x, 20-row strip) (raytracer.go:627-634). Launches on one context run in
+ * submission order: a launch on another stream than the previous launch
+ * waits for that launch to end. */
 int rt_render_rows_async(rt_context *ctx, int y0, int y1, void *d_rgba,
                          void *stream);
 
@@ -289,7 +300,9 @@ int rt_render_tile_rows_async(rt_context *ctx, int trow0, int trow_stride, int n
                               void *d_rgba, void *stream);
 
 /* Read (and optionally reset) the work counters accumulated on the device
- * since the last reset. Synchronises the given stream. */
+ * since the last reset. Synchronises the given stream. If the render
+ * watchdog stopped a wave (a kernel bug: a frame left unfinished) it returns
+ * RT_E_DEVICE and resets the counters whatever `reset` says. */
 int rt_read_stats(rt_context *ctx, void *stream, int reset, rt_stats *out);
 
 /* Device time (ms) of the most recent rt_render_rows_async on this context,
@@ -325,11 +338,26 @@ int rt_set_accel(rt_context *ctx, int flags);
  * lanes whose first lane adds them in sample order, 16 pixels per dequeue --
  * 4x shorter per-pixel latency, so deep branching glass trees do not leave a
  * few waves running long after the rest. RT_SCHED_AUTO (default): quads for
- * depth >= 7. Takes effect at the next rt_set_scene. */
+ * depth >= 7, and for launches that give each lane few pixels (a
+ * strong-scaling share of a frame). Takes effect at the next launch (the
+ * specialised kernel of the other schedule is compiled on first use). */
 #define RT_SCHED_AUTO 0
 #define RT_SCHED_PIXEL 1
 #define RT_SCHED_QUADS 2
 int rt_set_schedule(rt_context *ctx, int mode);
+
+/* Tile order (MI355X-specific; pixels and counters are identical either
+ * way). With enable != 0 (default) rt_set_scene also traces one centre sample
+ * per 8x8 tile of the frame at full depth and counts its rays; every launch
+ * then deals its tiles most expensive first (longest-processing-time-first),
+ * so the end of a launch is made of cheap tiles instead of the deep glass
+ * trees that otherwise keep a few waves running long after the rest. Scenes
+ * staged in LDS or with a BVH only (the estimate of a brute-force search over
+ * a large scene would cost too much). Applies to the current scene at once. */
+int rt_set_tile_order(rt_context *ctx, int enable);
+/* Whether the current scene has a tile order, and the estimate's wall time
+ * (ms) at scene setup. */
+int rt_tile_order_info(rt_context *ctx, int *active, double *estimate_ms);
 
 /* How the current scene is laid out for the device (bit flags), e.g. for
  * tests that must exercise one kernel flavour: RT_INFO_LDS the scene blob is

@@ -146,9 +146,118 @@ static inline double go_log(double x) {
     return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
 }
 
+/* math.Exp and math.Log as Go runs them on amd64 (math/exp_asm.go:
+ * haveArchExp, haveArchLog), restated from exp_amd64.s / log_amd64.s of the Go
+ * release go.mod:3 names (1.24.5). Those sources are not in /root/reference
+ * and there is no network: the restatement follows the published algorithm
+ * as recalled, and no reference fixture pins it (parity unpinned).
+ *
+ * exp_amd64.s (N. Shibata's method, from SLEEF): e = int32(trunc(x*log2(e)));
+ * r = (x - e*LN2U) - e*LN2L; r /= 16; y = e^r - 1 by a degree-8 Taylor series
+ * in Horner form; four doublings y = y*(y + 2) give e^(16r) - 1; + 1; times
+ * 2^e built from the exponent bits (two factors below the normal range).
+ * With AVX2+FMA (useFMA, i.e. any x86 server CPU of the last decade) the
+ * reduction and the series are fused multiply-adds: fma != 0. */
+static inline double go_bits_f64(uint64_t b) { double d; memcpy(&d, &b, 8); return d; }
+static inline double go_exp_amd64(double x, int fma_) {
+    const double LOG2E = 1.4426950408889634073599246810018920;
+    const double LN2U = 0.69314718055966295651160180568695068359375;
+    const double LN2L = 0.28235290563031577122588448175013436025525412068e-12;
+    const double Overflow = 7.09782712893384e+02;
+    /* exprodata: 1/2, 1, 2, 1/3!, 1/4!, ..., 1/8! */
+    static const double T[9] = {0.5, 1.0, 2.0, 1.6666666666666666667e-1, 4.1666666666666666667e-2,
+                                8.3333333333333333333e-3, 1.3888888888888888889e-3, 1.9841269841269841270e-4,
+                                2.4801587301587301587e-5};
+    uint64_t bx;
+    memcpy(&bx, &x, 8);
+    if ((bx & ~(1ull << 63)) >= 0x7FF0000000000000ull)  /* not finite: -Inf -> 0, NaN / +Inf -> x */
+        return bx == 0xFFF0000000000000ull ? 0.0 : x;
+    if (x > Overflow) return INFINITY;
+    const double t = LOG2E * x;
+    /* CVTTSD2SL: truncation; out of int32 range -> 0x80000000 */
+    const int32_t e = (t > -2147483649.0 && t < 2147483648.0) ? (int32_t)t : INT32_MIN;
+    const double fe = (double)e;
+    double r, p;
+    if (fma_) {
+        r = fma(-fe, LN2U, x); /* VFNMADD231SD */
+        r = fma(-fe, LN2L, r);
+    } else {
+        r = x - LN2U * fe;
+        r = r - LN2L * fe;
+    }
+    r = r * 0.0625;
+    p = T[8];
+    if (fma_) {
+        p = fma(r, p, T[7]); /* VFMADD213SD */
+        p = fma(r, p, T[6]);
+        p = fma(r, p, T[5]);
+        p = fma(r, p, T[4]);
+        p = fma(r, p, T[3]);
+        p = fma(r, p, T[0]);
+        p = fma(r, p, T[1]);
+    } else {
+        p = p * r + T[7];
+        p = p * r + T[6];
+        p = p * r + T[5];
+        p = p * r + T[4];
+        p = p * r + T[3];
+        p = p * r + T[0];
+        p = p * r + T[1];
+    }
+    double y = r * p;
+    for (int i = 0; i < 4; i++) y = y * (y + T[2]);
+    y = y + T[1];
+    /* return y * 2**e: biased exponent e + 1023 as bits */
+    int32_t b = e + 0x3FF;
+    if (b < 0) { /* denormal */
+        if (b < -52) return 0.0;
+        b += 0x3FE;
+        y = y * go_bits_f64((uint64_t)(uint32_t)b << 52);
+        return y * go_bits_f64(1ull << 52);
+    }
+    if ((uint32_t)b > 0x7FF) return INFINITY;
+    return y * go_bits_f64((uint64_t)(uint32_t)b << 52);
+}
+
+/* log_amd64.s: log.go's algorithm; Frexp is done on the bits without
+ * normalising a subnormal argument (exponent field 0 reads as 2^-1022 times
+ * 0.5 + mantissa) -- the only difference from go_log. */
+static inline double go_log_amd64(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+    const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+                 L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+                 L7 = 1.479819860511658591e-01;
+    uint64_t bx;
+    memcpy(&bx, &x, 8);
+    if ((bx & ~(1ull << 63)) == 0) return -INFINITY;           /* +-0 */
+    if ((int64_t)bx < 0) return NAN;                             /* negative (or -NaN) */
+    if (bx >= 0x7FF0000000000000ull) return x;                   /* +Inf, NaN */
+    double f1 = go_bits_f64((bx & 0x000FFFFFFFFFFFFFull) | 0x3FE0000000000000ull);
+    double k = (double)((int)((bx >> 52) & 0x7FF) - 0x3FE);
+    if (f1 < 0.70710678118654752440) { f1 *= 2; k -= 1; }
+    const double f = f1 - 1;
+    const double s = f / (2 + f);
+    const double s2 = s * s;
+    const double s4 = s2 * s2;
+    const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+    const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+    const double R = t1 + t2;
+    const double hfsq = 0.5 * f * f;
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+/* Which Exp/Log a fractional Pow runs (rt_scene.exp_mode, include/rt_abi.h):
+ * 0 = amd64 with FMA (the reference's deployment), 1 = amd64 without FMA,
+ * 2 = the portable exp.go / log.go. */
+static inline double go_exp_mode(double x, int mode) {
+    return mode == 2 ? go_exp(x) : go_exp_amd64(x, mode == 0);
+}
+static inline double go_log_mode(double x, int mode) { return mode == 2 ? go_log(x) : go_log_amd64(x); }
+
 /* math.Pow (pow.go). Integer exponents (specular n, Schlick 5) run the
- * Frexp/squaring loop; a fractional part goes through go_exp(yf*go_log(x)). */
-static inline double go_pow(double x, double y) {
+ * Frexp/squaring loop; a fractional part goes through Exp(yf*Log(x)) of the
+ * platform `mode` selects (go_exp_mode). */
+static inline double go_pow_m(double x, double y, int mode) {
     if (y == 0 || x == 1) return 1;
     if (y == 1) return x;
     if (isnan(x) || isnan(y)) return NAN;
@@ -168,7 +277,7 @@ static inline double go_pow(double x, double y) {
         return INFINITY;
     }
     if (isinf(x)) {
-        if (x < 0) return go_pow(1 / x, -y);
+        if (x < 0) return go_pow_m(1 / x, -y, mode);
         if (y < 0) return 0;
         if (y > 0) return INFINITY;
     }
@@ -187,7 +296,7 @@ static inline double go_pow(double x, double y) {
     int ae = 0;
     if (yf != 0) {
         if (yf > 0.5) { yf--; yi++; }
-        a1 = go_exp(yf * go_log(x));
+        a1 = go_exp_mode(yf * go_log_mode(x, mode), mode);
     }
     int xe;
     double x1 = go_frexp(x, &xe);
@@ -204,6 +313,7 @@ static inline double go_pow(double x, double y) {
     if (y < 0) { a1 = 1 / a1; ae = -ae; }
     return go_ldexp(a1, ae);
 }
+static inline double go_pow(double x, double y) { return go_pow_m(x, y, 2); }
 
 /* Cephes coefficients as in Go's sin.go / tan.go. */
 static const double go_sin_c[6] = {

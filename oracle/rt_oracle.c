@@ -126,6 +126,7 @@ typedef struct {
     const int32_t *code;
     const rt_material *mats;
     int nmats;
+    int exp_mode; /* rt_scene.exp_mode: the Exp/Log of a fractional Pow */
 } scene;
 
 typedef struct { vec3 origin, dir; } ray;
@@ -572,7 +573,7 @@ static vec3 compute_lighting(const scene *s, const hit *h, const hitex *x, ray r
         }
         if (s->lkind[li] == RT_LIGHT_SPOT) {          /* extension: cone falloff */
             double ca = v_dot(v_neg(ldir), s->ldir[li]);
-            lcol = v_scale(lcol, ca >= s->lcos[li] ? go_pow(ca, s->lexp[li]) : 0.0);
+            lcol = v_scale(lcol, ca >= s->lcos[li] ? go_pow_m(ca, s->lexp[li], s->exp_mode) : 0.0);
         }
         cnt->shadow++;
         if (in_shadow(s, h, x, ldir, dist, r, cnt)) continue;
@@ -580,7 +581,7 @@ static vec3 compute_lighting(const scene *s, const hit *h, const hitex *x, ray r
         vec3 diffuse = v_scale(lcol, ndl * mat->kd);
         vec3 H = v_norm(v_add(Vv, ldir));
         double spec = go_max(0, v_dot(x->nw, H));
-        vec3 specular = v_scale(lcol, mat->ks * go_pow(spec, mat->specular_exponent));
+        vec3 specular = v_scale(lcol, mat->ks * go_pow_m(spec, mat->specular_exponent, s->exp_mode));
         result = v_add(v_add(result, diffuse), specular);
     }
     return result;
@@ -705,6 +706,8 @@ static int convert_scene(const rt_scene *in, scene *s) {
     s->ambient = V(in->ambient[0], in->ambient[1], in->ambient[2]);
     s->bg0 = V(in->bg_start[0], in->bg_start[1], in->bg_start[2]);
     s->bg1 = V(in->bg_end[0], in->bg_end[1], in->bg_end[2]);
+    if (in->exp_mode < 0 || in->exp_mode > 2) return RT_E_INVALID;
+    s->exp_mode = in->exp_mode;
     const int ext = in->num_ext_lights > 0;
     if (ext && !in->ext_lights) return RT_E_INVALID;
     s->nlights = ext ? in->num_ext_lights : in->num_lights;
@@ -925,6 +928,9 @@ int oracle_surface_normal(const rt_scene *in, int idx, int face, const double po
 
 /* Go math restatements exposed for tests. */
 double oracle_go_pow(double x, double y) { return go_pow(x, y); }
+double oracle_go_pow_mode(double x, double y, int mode) { return go_pow_m(x, y, mode); }
+double oracle_go_exp_amd64(double x, int fma_) { return go_exp_amd64(x, fma_); }
+double oracle_go_log_amd64(double x) { return go_log_amd64(x); }
 double oracle_go_exp(double x) { return go_exp(x); }
 double oracle_go_log(double x) { return go_log(x); }
 double oracle_go_acos(double x) { return go_acos(x); }

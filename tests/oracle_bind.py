@@ -38,6 +38,12 @@ def lib():
         for fn in ("oracle_go_pow",):
             getattr(l, fn).argtypes = [C.c_double, C.c_double]
             getattr(l, fn).restype = C.c_double
+        l.oracle_go_pow_mode.argtypes = [C.c_double, C.c_double, C.c_int]
+        l.oracle_go_pow_mode.restype = C.c_double
+        l.oracle_go_exp_amd64.argtypes = [C.c_double, C.c_int]
+        l.oracle_go_exp_amd64.restype = C.c_double
+        l.oracle_go_log_amd64.argtypes = [C.c_double]
+        l.oracle_go_log_amd64.restype = C.c_double
         for fn in ("oracle_go_tan", "oracle_go_sin", "oracle_go_cos", "oracle_go_exp", "oracle_go_log"):
             getattr(l, fn).argtypes = [C.c_double]
             getattr(l, fn).restype = C.c_double

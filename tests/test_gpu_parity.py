@@ -621,8 +621,9 @@ def test_streamed_brute_force_c5_band_matches_oracle(ctx, spec_ctx):
 # sides): specular exponents and spot-light falloff.
 
 def test_device_exp_log_pow_equal_oracle_restatement():
-    """tests/hip/pow_check: device go_exp / go_log / go_pow vs the oracle's
-    host restatements, 4M random + edge inputs, bit for bit."""
+    """tests/hip/pow_check: device Exp / Log / Pow vs the oracle's host
+    restatements in every RT_EXP_* mode (Go's amd64 assembly with and without
+    FMA, the portable exp.go / log.go), 4M random + edge inputs, bit for bit."""
     import subprocess
     exe = os.path.join(os.path.dirname(__file__), "hip", "pow_check")
     if not os.path.exists(exe):
@@ -631,8 +632,10 @@ def test_device_exp_log_pow_equal_oracle_restatement():
     assert r.returncode == 0, r.stdout + r.stderr
     import json
     stats = json.loads(r.stdout.strip().splitlines()[-1])
-    assert stats["pow_mismatches"] == 0 and stats["exp_mismatches"] == 0 and stats["log_mismatches"] == 0
-    assert stats["fractional"] > 0.4 * stats["cases"], stats
+    assert [m["mode"] for m in stats["modes"]] == [0, 1, 2]
+    for m in stats["modes"]:
+        assert m["pow_mismatches"] == 0 and m["exp_mismatches"] == 0 and m["log_mismatches"] == 0, m
+        assert m["fractional"] > 0.4 * stats["cases"], stats
 
 
 def _fractional_scene(width, height, exps=(0.5, 2.5, 7.3, 33.3), spot_exp=2.7):
@@ -646,14 +649,16 @@ def _fractional_scene(width, height, exps=(0.5, 2.5, 7.3, 33.3), spot_exp=2.7):
                         width=width, height=height, bg_start=(0.0, 0.0, 0.0), bg_end=(0.5, 0.7, 1.0))
 
 
-def test_fractional_specular_and_spot_exponents_match_oracle(ctx, spec_ctx):
+@pytest.mark.parametrize("mode", [rt.abi.RT_EXP_AMD64_FMA, rt.abi.RT_EXP_AMD64, rt.abi.RT_EXP_PORTABLE])
+def test_fractional_specular_and_spot_exponents_match_oracle(ctx, spec_ctx, mode):
     """n in {0.5, 2.5, 7.3, 33.3} (specular) and a 2.7 spot falloff: the
-    fractional branch of math.Pow on the device equals the oracle's."""
-    packed = rt.scene.convert(_fractional_scene(160, 96))
+    fractional branch of math.Pow on the device equals the oracle's, with
+    each platform's Exp / Log (rt_scene.exp_mode)."""
+    packed = rt.scene.convert(replace(_fractional_scene(160, 96), exp_mode=mode))
     ref, ost = oracle_bind.render_rows(packed)
     for c in (ctx, spec_ctx):
         img, st = render(c, packed)
-        assert_same(img, ref, "fractional exponents")
+        assert_same(img, ref, "fractional exponents, exp mode %d" % mode)
         assert st.as_dict() == ost.as_dict()
 
 

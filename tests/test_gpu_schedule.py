@@ -1,0 +1,134 @@
+"""Work distribution on the device (needs an MI355X): the tile order dealt
+from the scene-setup cost estimate, work sharing at the tail of a launch
+(posted samples / refraction subtrees traced by idle lanes of the workgroup)
+and launches on several streams. None of them may change a byte or a
+counter: every case is checked against the CPU oracle (raytracer.go:589-682
+restated, tests/oracle_bind.py).
+"""
+import numpy as np
+import pytest
+
+import go_raytracer_amd as rt
+import oracle_bind
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    import torch
+    assert torch.cuda.is_available()
+    g = rt.RenderContext(0)
+    s = rt.RenderContext(0, specialize=True)
+    yield g, s
+    g.close()
+    s.close()
+
+
+def render(ctx, packed):
+    ctx.set_scene(packed)
+    ctx.read_stats(reset=True)
+    img = ctx.render()
+    st = ctx.read_stats(reset=True)
+    return img, st
+
+
+def assert_same(img, ref, what):
+    if not np.array_equal(img, ref):
+        bad = np.argwhere((img != ref).any(axis=-1))
+        y, x = bad[0]
+        raise AssertionError("%s: %d pixels differ; first at (x=%d,y=%d) gpu=%s oracle=%s"
+                             % (what, len(bad), x, y, img[y, x], ref[y, x]))
+
+
+CASES = {
+    # deep binary glass trees (raytracer.go:512-556) in few pixels per lane:
+    # most lanes are idle from the start, so nearly every sample and pending
+    # refraction child is posted to the board
+    "c4_small": lambda: rt.configs.c4(width=72, height=40),
+    "c3_small": lambda: rt.configs.c3(width=96, height=56),
+    "canned_small": lambda: rt.configs.canned(width=64, height=40),
+    "c4csg_small": lambda: rt.configs.c4csg(width=64, height=48),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_tile_order_and_sharing_match_oracle(ctxs, case):
+    packed = rt.scene.convert(CASES[case]())
+    ref, ost = oracle_bind.render_rows(packed)
+    for c in ctxs:
+        try:
+            for order in (True, False):
+                c.set_tile_order(order)
+                for mode in (rt.abi.RT_SCHED_PIXEL, rt.abi.RT_SCHED_QUADS):
+                    c.set_schedule(mode)
+                    img, st = render(c, packed)
+                    what = "%s order=%s schedule=%d" % (case, order, mode)
+                    assert_same(img, ref, what)
+                    assert st.as_dict() == ost.as_dict(), what
+        finally:
+            c.set_tile_order(True)
+            c.set_schedule(rt.abi.RT_SCHED_AUTO)
+
+
+def test_cost_estimate_leaves_counters_alone(ctxs):
+    """The scene-setup estimate launch traces rays too; they must not reach
+    the frame's counters."""
+    g, _ = ctxs
+    packed = rt.scene.convert(rt.configs.c3(width=128, height=72))
+    g.read_stats(reset=True)
+    g.set_scene(packed)
+    active, ms = g.tile_order_info()
+    assert active and ms > 0
+    st = g.read_stats(reset=True)
+    assert st.total_rays() == 0 and st.shaded_hits == 0
+    ref, ost = oracle_bind.render_rows(packed)
+    img = g.render()
+    st = g.read_stats(reset=True)
+    assert_same(img, ref, "c3 after estimate")
+    assert st.as_dict() == ost.as_dict()
+
+
+def test_interleaved_shares_with_order_match_full_frame(ctxs):
+    """Strong-scaling shares (tile rows r, r + N, ...) each get their own
+    tile order; gathered, they are the oracle's frame."""
+    import torch
+    _, s = ctxs
+    args = rt.configs.c4(width=160, height=96)
+    packed = rt.scene.convert(args)
+    ref, ost = oracle_bind.render_rows(packed)
+    s.set_scene(packed)
+    s.read_stats(reset=True)
+    world = 3
+    nt, K = rt.dist.tile_rows(packed.height, world)
+    slabs = torch.zeros((world, K * 8, packed.width, 4), dtype=torch.uint8, device="cuda:0")
+    for r in range(world):
+        n = max(0, min(K, (nt - r + world - 1) // world))
+        s.render_tile_rows_async(r, world, n, slabs[r, : n * 8])
+    torch.cuda.synchronize()
+    img = rt.dist.deinterleave(slabs, packed.height).cpu().numpy()
+    st = s.read_stats(reset=True)
+    assert_same(img, ref, "interleaved shares")
+    assert st.as_dict() == ost.as_dict()
+
+
+def test_launches_on_alternating_streams(ctxs):
+    """Launches alternate between two sets of queue heads; a launch on
+    another stream waits for the previous one, so back-to-back launches on
+    different streams render every row."""
+    import torch
+    g, _ = ctxs
+    packed = rt.scene.convert(rt.configs.c2(width=200, height=120))
+    ref, ost = oracle_bind.render_rows(packed)
+    g.set_scene(packed)
+    g.read_stats(reset=True)
+    streams = [torch.cuda.Stream(device=0) for _ in range(3)]
+    outs = [torch.zeros((120, 200, 4), dtype=torch.uint8, device="cuda:0") for _ in range(6)]
+    for k, o in enumerate(outs):
+        g.render_rows_async(0, 120, o, stream=streams[k % 3])
+    torch.cuda.synchronize()
+    for k, o in enumerate(outs):
+        assert_same(o.cpu().numpy(), ref, "launch %d" % k)
+    st = g.read_stats(reset=True)
+    for key, v in ost.as_dict().items():
+        assert st.as_dict()[key] == 6 * v, key

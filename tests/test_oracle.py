@@ -145,6 +145,44 @@ def test_go_exp_log_restatement():
         assert _ulps(l.oracle_go_log(x), math.log(x)) <= 1, x
 
 
+def test_go_exp_amd64_restatement():
+    """math.Exp as Go runs it on amd64 (exp_amd64.s, with and without FMA;
+    recalled): special cases, overflow / underflow thresholds,
+    within 4 ulp of libm, and genuinely different from the portable exp.go in
+    the last bit of a sizeable share of inputs -- which is why the platform
+    is a scene option (rt_scene.exp_mode)."""
+    l = oracle_bind.lib()
+    for f in (0, 1):
+        e = lambda x: l.oracle_go_exp_amd64(x, f)  # noqa: E731
+        assert e(0.0) == 1.0 and e(float("-inf")) == 0.0 and e(float("inf")) == float("inf")
+        assert math.isnan(e(float("nan"))) and e(709.79) == float("inf") and e(-1e10) == 0.0
+        assert e(-745.0) == 5e-324 and e(-740.0) == 4.2e-322  # the two-factor denormal path
+        rng = np.random.default_rng(7 + f)
+        for x in rng.uniform(-700, 700, 20000):
+            assert _ulps(e(x), math.exp(x)) <= 4, x
+    rng = np.random.default_rng(11)
+    xs = rng.uniform(-30, 30, 20000)
+    fma_vs_plain = sum(l.oracle_go_exp_amd64(x, 1) != l.oracle_go_exp_amd64(x, 0) for x in xs)
+    amd64_vs_portable = sum(l.oracle_go_exp_amd64(x, 1) != l.oracle_go_exp(x) for x in xs)
+    assert 0 < fma_vs_plain < 0.05 * len(xs) and amd64_vs_portable > 0.1 * len(xs)
+    # log_amd64.s: log.go's algorithm (bit-level Frexp: equal for normal inputs)
+    for x in np.exp(rng.uniform(-700, 700, 5000)):
+        assert l.oracle_go_log_amd64(x) == l.oracle_go_log(x), x
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_go_pow_modes(mode):
+    """Pow with each platform's Exp / Log: integer exponents never reach
+    Exp (identical in every mode); fractional ones stay within Pow's error."""
+    l = oracle_bind.lib()
+    rng = np.random.default_rng(mode)
+    for x in rng.uniform(1e-3, 1.0, 2000):
+        for y in (2.0, 5.0, 40.0):
+            assert l.oracle_go_pow_mode(x, y, mode) == l.oracle_go_pow(x, y)
+        got, want = l.oracle_go_pow_mode(x, 7.3, mode), x ** 7.3
+        assert abs(got - want) <= 64 * abs(want) * 2.0 ** -52, (x, got, want)
+
+
 @pytest.mark.parametrize("y", [0.5, 2.5, 7.3, 33.3, -1.5, 0.75])
 def test_go_pow_fractional_exponents(y):
     """Pow's fractional part: yf > 0.5 folds to yf - 1 (yi + 1), then
