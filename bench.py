@@ -147,6 +147,38 @@ def cpu_baseline(packed, threads, budget_s=10.0):
     return out
 
 
+def side_config(pkg, name, dev, specialize, steps=10, warmup=2):
+    """One GPU, whole frames of another config (the C3 line's companion: C3 as
+    BASELINE.json states it, with the cone the reference lacks): value,
+    ms/frame and the reference-work roofline fraction."""
+    import torch
+    rargs = pkg.configs.CONFIGS[name]()
+    packed = pkg.scene.convert(rargs)
+    ctx = pkg.RenderContext(dev.index, specialize=specialize)
+    ctx.set_scene(packed)
+    buf = torch.zeros((packed.height, packed.width, 4), dtype=torch.uint8, device=dev)
+    for _ in range(warmup):
+        ctx.render_rows_async(0, packed.height, buf)
+    torch.cuda.synchronize()
+    ctx.read_stats(reset=True)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record()
+        ctx.render_rows_async(0, packed.height, buf)
+        e1.record()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = ctx.read_stats(reset=True)
+    kavg = sum(a.elapsed_time(b) for a, b in evs) / steps
+    flops = pkg.abi.algorithmic_flops(st, len(rargs.lights)) / steps
+    ctx.close()
+    return {"workload": "%s: %s" % (name, pkg.configs.WORKLOADS[name]), "value": round(st.total_rays() / dt / 1e6, 2),
+            "unit": "Mrays/s", "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms": round(kavg, 4),
+            "rays_per_step": int(st.total_rays() / steps),
+            "frac": round(flops / (kavg * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4), "parity": "unpinned (cone: contest extension)"}
+
+
 def main():
     args = parse()
     pkg = load_package()
@@ -177,6 +209,7 @@ def main():
     ctx.set_scene(packed)
     spec_active, spec_ms = ctx.specialized()
     order_active, order_ms = ctx.tile_order_info()
+    bvh = bool(ctx.scene_info() & pkg.abi.RT_INFO_BVH)
     mode = "frame" if args.scaling == "weak" else args.shard
     band = None
     if args.rows:
@@ -255,8 +288,14 @@ def main():
                        "spec_compile_ms": round(spec_ms, 1),
                        "tile_order_ms": round(order_ms, 2) if order_active else None},
             "roofline": {"bound": "valu-fp64", "achieved": round(achieved_tf, 3), "peak": PEAK_FP64_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
-                         "frac_nofma_ceiling": round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),
+                         "unit": "TFLOP/s",
+                         # with a BVH the kernel skips most of the reference's
+                         # Intersect calls, so reference work per second is no
+                         # utilisation (it can exceed 1): null, and the executed
+                         # fraction (PMC) carries the roofline instead
+                         "frac": None if bvh else round(achieved_tf / PEAK_FP64_TFLOPS, 4),
+                         "reference_work_frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
+                         "frac_nofma_ceiling": None if bvh else round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),
                          "kernel_ms": round(kavg, 4), "flops_per_launch": int(flops_per_launch),
                          "hbm_out_gbs": round(out_bytes / (kavg * 1e-3) / 1e9, 2) if kavg > 0 else None,
                          "traffic": None, "traffic_source": None},
@@ -266,6 +305,10 @@ def main():
         key = args.config + ("_bf" if args.accel == "none" else "") + \
             ("_rows%d-%d" % band if band else "")
         ex, exsrc = pmc_executed(key) if (world == 1 and not args.width and not args.height) else (None, None)
+        if ex is not None and ex.get("kernel_src") != pkg.render.kernel_source_id():
+            # counters of another kernel build: not quoted as this run's
+            line["roofline"]["pmc_stale"] = exsrc
+            ex = None
         if ex is not None and kavg > 0:
             ex_tf = ex["executed_fp64_flops"] / (kavg * 1e-3) / 1e12
             line["roofline"].update({
@@ -280,6 +323,8 @@ def main():
         if tb is not None and world == 1 and not args.width and not args.height and not band:
             line["roofline"]["traffic"] = int(tb)
             line["roofline"]["traffic_source"] = src
+        if world == 1 and args.config == "c3" and not (args.width or args.height or band):
+            line["c3cone"] = side_config(pkg, "c3cone", dev, args.specialize == "on")
         if world == 1 and args.cpu_baseline == "auto":
             line["cpu_baseline"] = cpu_baseline(packed, args.cpu_threads)
         print(json.dumps(line), flush=True)

@@ -446,10 +446,11 @@ struct SpecKey {
   int pow_bits = 7;                      // unrolled specular powering steps
   int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
   int quads = 0;                         // pixel quads (use_quads)
+  int share = 0;                         // work sharing at the tail (rt_set_work_sharing): -DRT_SHARE=1
   std::string str() const {
     return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
            std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits) +
-           ":" + std::to_string(nocull) + ":" + std::to_string(quads);
+           ":" + std::to_string(nocull) + ":" + std::to_string(quads) + ":" + std::to_string(share);
   }
 };
 
@@ -490,6 +491,7 @@ struct rt_context {
   // tile is traced (estimate launch); launches then deal their tiles most
   // expensive first, so the end of a launch is made of cheap tiles.
   bool order_on = true;
+  bool share_on = false;  // rt_set_work_sharing (specialised kernels only)
   unsigned int* est = nullptr;              // device: rays traced per frame tile
   size_t est_cap = 0;                       // tiles est can hold
   unsigned long long* est_stats = nullptr;  // the estimate launch's counters (discarded)
@@ -755,6 +757,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   if (sk.nlights > 0) defs.push_back("-DRT_SPEC_NLIGHTS=" + std::to_string(sk.nlights));
   defs.push_back("-DRT_SPEC_POWBITS=" + std::to_string(sk.pow_bits));
   if (sk.nocull) defs.push_back("-DRT_CULL=0");
+  if (sk.share) defs.push_back("-DRT_SHARE=1");
   std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
   for (const auto& d : defs) opts.push_back(d.c_str());
   // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only)
@@ -842,6 +845,7 @@ int spec_prepare(rt_context* c) {
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
   sk.quads = use_quads(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus) ? 1 : 0;
+  sk.share = c->share_on ? 1 : 0;
   c->spec_key = sk;
   c->spec_alt_fn = nullptr;
   std::lock_guard<std::mutex> lock(g_spec_mu);
@@ -923,7 +927,8 @@ int rt_scene_info(rt_context* c, int* flags) {
   const DevScene& s = c->sc;
   const bool lds = scene_in_lds(s);
   *flags = (lds ? RT_INFO_LDS : 0) | (s.use_bvh ? RT_INFO_BVH : 0) | (s.has_csg ? RT_INFO_CSG : 0) |
-           ((!lds && !s.use_bvh && !s.has_csg) ? RT_INFO_STREAM : 0);
+           ((!lds && !s.use_bvh && !s.has_csg) ? RT_INFO_STREAM : 0) |
+           ((c->spec_fn && c->spec_key.share) ? RT_INFO_WAVEFRONT : 0) | (c->tile_cost.empty() ? 0 : RT_INFO_ORDERED);
   return RT_OK;
 }
 
@@ -1528,14 +1533,11 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // per-wave object-record stream buffers (global linear scenes, RT_STREAM)
   const int jump_off = qmask_off + 16;  // after the drained-head mask: the sample-0 jump rows
   const int board_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);  // work-sharing board (RT_SHARE)
-  const int stream_off = board_off + (RT_SHARE ? BOARD_BYTES : 0);
   // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
   // loads instead: no stream buffers)
   // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)
   static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
-  const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
-  int shmem = frames_off;
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
   const bool quads = !est && use_quads(c->sched, s, launch_pixels, c->cus);
   const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
@@ -1544,6 +1546,11 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     int rc = spec_for(c, quads, &spec);
     if (rc != RT_OK) return rc;
   }
+  // the board is in LDS only for a kernel compiled with work sharing
+  const bool share = spec && c->spec_key.share;
+  const int stream_off = board_off + (share ? BOARD_BYTES : 0);
+  const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
+  int shmem = frames_off;
   auto occupancy = [&](int bytes) {
     int n = 0;
     if (spec) {
@@ -1719,7 +1726,10 @@ static int estimate_costs(rt_context* c) {
     HIP_TRY(hipMalloc((void**)&c->est, n * sizeof(unsigned int)));
     c->est_cap = n;
   }
-  if (!c->est_stats) HIP_TRY(hipMalloc((void**)&c->est_stats, sizeof(unsigned long long) * 64));
+  if (!c->est_stats) {
+    HIP_TRY(hipMalloc((void**)&c->est_stats, sizeof(unsigned long long) * 64));
+    HIP_TRY(hipMemset(c->est_stats, 0, sizeof(unsigned long long) * 64));
+  }
   const auto t0 = std::chrono::steady_clock::now();
   HIP_TRY(hipMemset(c->est, 0, n * sizeof(unsigned int)));
   int rc = launch(c, 0, s.height, 0, 0, 0, nullptr, nullptr, true);
@@ -1734,6 +1744,12 @@ static int estimate_costs(rt_context* c) {
   c->order_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   c->timed = false;
   return RT_OK;
+}
+
+int rt_set_work_sharing(rt_context* c, int enable) {
+  if (!c) return fail(RT_E_INVALID, "rt_set_work_sharing: NULL context");
+  c->share_on = enable != 0;
+  return c->has_scene ? spec_prepare(c) : RT_OK;
 }
 
 int rt_set_tile_order(rt_context* c, int enable) {
@@ -1841,6 +1857,12 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
                   cd[1], 100.0 * cd[1] / cd[0], (double)cd[2] / cd[0]);
       }
 #endif
+      {
+        unsigned long long sh[6];
+        HIP_TRY(hipMemcpy(sh, c->stats + ST_SHDIAG, sizeof sh, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[share] posted samples %llu subtrees %llu, claims %llu, reclaims %llu, waits %llu, idle polls %llu\n",
+                sh[0], sh[1], sh[2], sh[3], sh[4], sh[5]);
+      }
       fprintf(stderr, "[waves] lifetime mean %.4g cycles, max %.4g cycles (mean/max %.3f)\n",
               (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches), (double)bd[7],
               (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches) / (double)std::max(1ull, bd[7]));

@@ -143,7 +143,16 @@ enum { QSET = QHEADS * QSTRIDE /* u32 per launch set of heads */ };
 #endif
 enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
-       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32, ST_WATCHDOG = 63 };  // (stats buffer: 64 entries)
+       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32, ST_SHDIAG = 48, ST_WATCHDOG = 63 };
+// Diagnostic build (RT_PHASE_TIMING): work-sharing events, ST_SHDIAG + k:
+// 0 samples posted, 1 subtrees posted, 2 claims, 3 reclaims, 4 waits, 5 rounds
+// a wave spent polling idle
+enum { SH_POST_S = 0, SH_POST_T = 1, SH_CLAIM = 2, SH_RECLAIM = 3, SH_WAIT = 4, SH_SPIN = 5 };
+#ifdef RT_PHASE_TIMING
+#define SHDIAG(k) atomicAdd(P.stats + ST_SHDIAG + (k), 1ull)
+#else
+#define SHDIAG(k) (void)0
+#endif  // (stats buffer: 64 entries)
 enum { S_IDLE = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };  // S_DONE: sample colour held for the quad
 #ifndef RT_LDS_MAX
 #define RT_LDS_MAX (40 * 1024)
@@ -1048,7 +1057,10 @@ __device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ?
 // Frame flags (packed with the material index): packed = material << PK_MAT |
 // board slot << PK_SLOT | flags. FL_FORKED: the pending refraction child was
 // posted to the workgroup's board (slot PK_SLOT) for another lane to trace.
-enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16, FL_FORKED = 32 };
+// FL_TASK: a sentinel below a claimed subtree -- its colour goes to slot
+// PK_SLOT (the subtree runs at its own absolute levels, so the depth limit
+// and the frame layout are those of the owner's tree).
+enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16, FL_FORKED = 32, FL_TASK = 64 };
 enum { PK_SLOT = 8, PK_MAT = 16 };
 
 // ---------------------------------------------------------------------------
@@ -1072,12 +1084,16 @@ enum { PK_SLOT = 8, PK_MAT = 16 };
 // Slot state lives in two 64-bit LDS masks (posted, delivered) changed by
 // atomics; a wave allocates and frees only the slots of its own range.
 // ---------------------------------------------------------------------------
+// Off by default: in this register-saturated kernel (168 VGPRs at 3 waves per
+// SIMD) the board's code costs C3 ~10 % in every round (spills, +5 % VALU and
+// +13 % SALU instructions, PMC), more than the tail gains; rt_set_work_sharing
+// compiles it into a context's specialised kernel.
 #ifndef RT_SHARE
-#ifdef RT_COST_MAP
-#define RT_SHARE 0  // the cost-map diagnostic charges a pixel's work to its own lane
-#else
-#define RT_SHARE 1
+#define RT_SHARE 0
 #endif
+#ifdef RT_COST_MAP
+#undef RT_SHARE
+#define RT_SHARE 0  // the cost-map diagnostic charges a pixel's work to its own lane
 #endif
 #ifndef RT_SHARE_SPINS
 #define RT_SHARE_SPINS (1 << 16)  // idle rounds (s_sleep'd) a drained wave waits for work before leaving
@@ -1089,7 +1105,11 @@ enum { PK_SLOT = 8, PK_MAT = 16 };
 #ifndef RT_SHARE_SAMPLES
 #define RT_SHARE_SAMPLES 1  // post unstarted samples (serial schedule), not only refraction subtrees
 #endif
-enum { NSLOT = 64, SLOTS_PER_WAVE = NSLOT / WAVES_PER_WG, S_WAIT = 4 };
+enum { NSLOT = 64, SLOTS_PER_WAVE = NSLOT / WAVES_PER_WG, S_WAIT = 4, S_RESUME = 5 };
+// S_ADV (serial samples): the lane finished a sample (its colour added to sum);
+// the next one is chosen at the top of the main loop (advance_sample), in one
+// place rather than in each unwind site (instruction-cache footprint).
+enum { S_ADV = 6 };
 struct Board {
   unsigned long long post;           // slots holding a task nobody has claimed
   unsigned long long done;           // slots whose colour has been delivered
@@ -1100,8 +1120,16 @@ struct Board {
   // subtree task: the pending refraction ray (origin, direction), read by the
   // helper when it claims the slot; then the delivered colour (res = ray[0..2])
   double ray[NSLOT][6];
-  int meta[NSLOT][2];  // subtree: depth offset, 0; sample: x | k << 16 | 1 << 30, y
+  int meta[NSLOT][2];  // subtree: level of the child, 0; sample: x | k << 16 | 1 << 30, y
+  // Per lane, the rarely used sample bookkeeping (kept out of the registers
+  // of a kernel that uses all of them): bits 0-2 own_end (the lane traces
+  // samples [0, own_end) of its pixel itself), 3-9 claimed sample task's slot
+  // + 1 (0: its own pixel), 10-27 the slots of posted samples 1..3.
+  uint32_t lw[WG];
 };
+__device__ __forceinline__ int lw_own_end(uint32_t w) { return (int)(w & 7u); }
+__device__ __forceinline__ int lw_task(uint32_t w) { return (int)((w >> 3) & 127u) - 1; }
+__device__ __forceinline__ int lw_fork(uint32_t w, int k) { return (int)((w >> (10 + 6 * (k - 1))) & 63u); }
 enum { BOARD_BYTES = (int)sizeof(Board), META_SAMPLE = 1 << 30 };
 #define RT_WG_SCOPE __HIP_MEMORY_SCOPE_WORKGROUP
 __device__ __forceinline__ bool board_reclaim(Board* b, int q) {  // owner: take back a task nobody claimed
@@ -1314,7 +1342,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       Bd->post = 0ull;
       Bd->done = 0ull;
       Bd->nidle = 0;
-      Bd->nactive = 0;
+      Bd->nactive = WAVES_PER_WG;  // every wave starts busy (my_active)
     }
     if (threadIdx.x < WAVES_PER_WG) Bd->wfree[threadIdx.x] = (1u << SLOTS_PER_WAVE) - 1u;
   }
@@ -1442,16 +1470,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   bool need_gen = false;  // lane waits for its next sample ray
   int px = 0, py = 0, sample = 0, sp = 0;
   unsigned int pout = 0;  // output pixel index
-  // work sharing (RT_SHARE): the lane's own samples are [0, own_end) -- the
-  // rest were posted, sample k to board slot (sfork >> 8k) & 63; pend bit L:
-  // frame L holds a pending refraction child not yet posted; task >= 0: the
-  // lane runs a claimed task for slot `task`, its tree rooted at level dbase
-  int own_end = 4, task = -1, dbase = 0;
-  uint32_t sfork = 0u, pend = 0u;
+  // work sharing (RT_SHARE): per-lane sample bookkeeping in Bd->lw (Board)
   const int wave = (int)(threadIdx.x >> 6);
   int my_idle = 0, spins = 0;  // wave-uniform: idle lanes this wave reports, idle rounds
-  bool my_active = false;      // wave-uniform: counted in Bd->nactive
-  bool resumed = false;        // a waiting owner's helper delivered (taken by the TRACE pass's unwind)
+  bool my_active = true;       // wave-uniform: counted in Bd->nactive
+  // wave-uniform: the tail has begun for this wave (it drained the queue, or
+  // another wave of the group reported idle lanes); until then the board is
+  // only looked at every 4th round
+  bool sh_live = false;
   int hit_i = 0, hit_f = 0;
   double hit_t = 0.0;
   Pcg rng{0, 0};
@@ -1508,13 +1534,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // The board slot a waiting owner (S_WAIT) waits on: its posted sample
   // `sample` (at sp == 0), else the posted refraction child of frame sp - 1.
   auto wait_slot = [&]() -> int {
-    if (!QD && sp == 0) return (int)((sfork >> (8 * sample)) & 63u);
+    if (!QD && sp == 0) return lw_fork(Bd->lw[threadIdx.x], sample);
     return (int)((__double_as_longlong(core_ld(sp - 1, 4)) >> PK_SLOT) & 63);
   };
   // Serial samples: account sample `sample` onwards after the lane finished
   // the one before -- run it (own), take a helper's colour, reclaim a posted
   // sample nobody claimed, or wait; quantise once all 4 are summed.
-  auto advance_sample = [&]() {
+  auto advance_sample = [&](uint32_t w) {  // w: the lane's Bd->lw word
     for (;;) {
       if (P.est_out && sample == 1) {  // cost estimate: one sample per tile
         state = S_IDLE;
@@ -1534,22 +1560,24 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         state = S_IDLE;
         return;
       }
-      if (!RT_SHARE || sample < own_end) {
+      if (!RT_SHARE || __builtin_expect(sample < lw_own_end(w), 1)) {
         need_gen = true;  // next sample ray, generated in one uniform block
         state = S_TRACE;
         return;
       }
-      const int q = (int)((sfork >> (8 * sample)) & 63u);
+      const int q = lw_fork(w, sample);
       if (board_reclaim(Bd, q)) {  // nobody took it: trace it here
+        SHDIAG(SH_RECLAIM);
         board_free(Bd, q);
-        own_end = sample + 1;
+        Bd->lw[threadIdx.x] = (w & ~7u) | (uint32_t)(sample + 1);  // own_end = sample + 1
         rng = sample_rng(px, py, sample);
         need_gen = true;
         state = S_TRACE;
         return;
       }
       if (!board_done(Bd, q)) {
-        state = S_WAIT;  // (the slot is found again from sfork: wait_slot)
+        SHDIAG(SH_WAIT);
+        state = S_WAIT;  // (the slot is found again from Bd->lw: wait_slot)
         return;
       }
       sum = add(sum, board_take(Bd, q));  // raytracer.go:651, in sample order
@@ -1565,18 +1593,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     while (__any(have_res)) {
       if (have_res) {
         if (sp == 0) {
-          if (RT_SHARE && task >= 0) {  // a claimed task: hand the colour to its owner
-            board_deliver(Bd, task, res);
-            task = -1;
-            dbase = 0;
-            state = S_IDLE;
-          } else if constexpr (QD) {
+          if constexpr (QD) {
             sum = res;  // this sample's colour, summed by the quad's first lane (main loop)
             state = S_DONE;
           } else {
-            sum = add(sum, res);  // raytracer.go:651
+            // raytracer.go:651 (a claimed sample's helper starts from sum = -0:
+            // -0 + c == c for every c, so sum is exactly its colour)
+            sum = add(sum, res);
             sample++;
-            advance_sample();
+            state = S_ADV;
           }
           have_res = false;
         } else {
@@ -1587,14 +1612,19 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           else
             packed = __double_as_longlong(core_ld(sp - 1, 4));
           int fl = (int)(packed & 0xff);
-          if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
+          if (RT_SHARE && __builtin_expect((fl & FL_TASK) != 0, 0)) {  // a claimed subtree is done: hand its colour to the owner
+            board_deliver(Bd, (int)((packed >> PK_SLOT) & 63), res);
+            sp = 0;
+            state = S_IDLE;
+            have_res = false;
+          } else if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
             // reflection child done; trace the pending refraction child
             st3(ext(sp - 1), 0, res);
             core_st(sp - 1, 4, __longlong_as_double(packed | FL_STAGE));
-            if (RT_SHARE) pend &= ~(1u << (sp - 1));
-            if (RT_SHARE && (fl & FL_FORKED)) {
+            if (RT_SHARE && __builtin_expect((fl & FL_FORKED) != 0, 0)) {
               const int q = (int)((packed >> PK_SLOT) & 63);
               if (board_reclaim(Bd, q)) {  // nobody took it: trace it here
+                SHDIAG(SH_RECLAIM);
                 board_free(Bd, q);
                 ray.o = ld3(ext(sp - 1), 3);
                 ray.d = ld3(ext(sp - 1), 6);
@@ -1603,6 +1633,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               } else if (board_done(Bd, q)) {
                 res = board_take(Bd, q);  // the next round combines (FL_STAGE set)
               } else {
+                SHDIAG(SH_WAIT);
                 state = S_WAIT;  // (the slot is found again from the frame: wait_slot)
                 have_res = false;
               }
@@ -1662,6 +1693,22 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (++guard_iters > (1u << 26)) {
       if (lane == 0) atomicAdd(P.stats + ST_WATCHDOG, 1ull);
       break;
+    }
+    // ---- serial samples: a lane that finished a sample goes on with the next
+    // one (or hands a claimed sample's colour to its owner) ----
+    if constexpr (!QD) {
+      if (__any(state == S_ADV)) {
+        if (state == S_ADV) {
+          const uint32_t w = RT_SHARE ? Bd->lw[threadIdx.x] : 4u;
+          if (RT_SHARE && __builtin_expect(lw_task(w) >= 0, 0)) {
+            board_deliver(Bd, lw_task(w), sum);
+            Bd->lw[threadIdx.x] = 0u;
+            state = S_IDLE;
+          } else {
+            advance_sample(w);
+          }
+        }
+      }
     }
     // ---- quads whose 4 samples are all done: the first lane adds the
     // colours in sample order (raytracer.go:651) and quantises
@@ -1739,10 +1786,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           rng = pcg_jump(Pcg{0xDEADULL ^ (uint64_t)px, 0xBEEFULL ^ (uint64_t)(py - ry)}, jrows[ry * 4],
                          jrows[ry * 4 + 1], jrows[ry * 4 + 2], jrows[ry * 4 + 3]);
           sample = 0;
-          own_end = 1;
+          if (RT_SHARE) Bd->lw[threadIdx.x] = 1u;  // own_end = 1
           sum = mk(0, 0, 0);
           sp = 0;
-          pend = 0u;
           need_gen = true;
           state = S_TRACE;
         }
@@ -1779,34 +1825,49 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sum = mk(0, 0, 0);
           sp = 0;
-          own_end = 4;
-          pend = 0u;
+          if (RT_SHARE) Bd->lw[threadIdx.x] = 4u;  // own_end = 4, nothing posted
           need_gen = true;
           state = S_TRACE;
         }
       }
       pool_next += take;
     }
-    if constexpr (RT_SHARE) {
+    if (RT_SHARE && !sh_live && !exhausted && (guard_iters & 3u) == 0u)
+      sh_live = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&Bd->nidle, __ATOMIC_RELAXED, RT_WG_SCOPE)) > 0;
+    if (RT_SHARE && !sh_live && exhausted) sh_live = true;
+    if (RT_SHARE && !sh_live) {
+      // steady state: the refill left no lane idle (else the queue is drained)
+    } else if constexpr (RT_SHARE) {
       // ---- work sharing within the workgroup (see Board) ----
       // (a) owners whose helper delivered take the colour; it is propagated
       // by the TRACE pass's unwind (a posted sample is added in sample order
       // at sp == 0, a posted refraction child combined at its frame)
-      if (__any(state == S_WAIT)) {
-        resumed = state == S_WAIT && board_done(Bd, wait_slot());
+      if (__builtin_expect(__any(state == S_WAIT), 0)) {
+        if (state == S_WAIT && board_done(Bd, wait_slot())) state = S_RESUME;
       }
       // (b) owners post work they have not started, while drained waves of
       // the group have idle lanes to take it
       const int nid = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&Bd->nidle, __ATOMIC_RELAXED, RT_WG_SCOPE));
-      if (nid > 0) {
-        const uint64_t pm = __hip_atomic_load(&Bd->post, __ATOMIC_RELAXED, RT_WG_SCOPE);
-        const int want = nid - (int)__popcll(((uint64_t)__builtin_amdgcn_readfirstlane((int)(pm >> 32)) << 32) |
-                                             (uint32_t)__builtin_amdgcn_readfirstlane((int)pm));
+      const uint64_t pmp = nid > 0 ? __hip_atomic_load(&Bd->post, __ATOMIC_RELAXED, RT_WG_SCOPE) : 0ull;
+      const int want = nid - (int)__popcll(((uint64_t)__builtin_amdgcn_readfirstlane((int)(pmp >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((int)pmp));
+      if (__builtin_expect(want > 0, 0)) {
         const bool busy_lane = state == S_TRACE || state == S_SHADE || state == S_WAIT;
-        const bool cs = !QD && RT_SHARE_SAMPLES && busy_lane && task < 0 && own_end - 1 > sample;  // an unstarted own sample
-        const bool cand = cs || (busy_lane && pend != 0u);
+        // candidates: an unstarted own sample (serial samples), else the
+        // shallowest frame whose refraction child is pending and not posted
+        // (frames above a claimed subtree's sentinel only)
+        const uint32_t w = busy_lane ? Bd->lw[threadIdx.x] : 0u;
+        const bool cs = !QD && RT_SHARE_SAMPLES && busy_lane && lw_task(w) < 0 && lw_own_end(w) - 1 > sample;
+        int L = -1;
+        if (busy_lane && !cs)
+          for (int l = sp - 1; l >= 0; l--) {
+            const int f = (int)(__double_as_longlong(core_ld(l, 4)) & 0xff);
+            if (f & FL_TASK) break;
+            if ((f & (FL_HASR | FL_HAST | FL_STAGE | FL_FORKED)) == (FL_HASR | FL_HAST)) L = l;
+          }
+        const bool cand = cs || L >= 0;
         const uint64_t cm = __ballot(cand);
-        if (want > 0 && cm) {
+        if (cm) {
           const uint32_t wf = (uint32_t)__builtin_amdgcn_readfirstlane(
               (int)__hip_atomic_load(&Bd->wfree[wave], __ATOMIC_RELAXED, RT_WG_SCOPE));
           const int npost = min(min((int)__popcll(cm), (int)__popc(wf)), want);
@@ -1817,13 +1878,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             if (cand && rk < npost) {
               const int q = wave * SLOTS_PER_WAVE + nth_bit(wf, rk);
               if (cs) {  // the last of the lane's unstarted samples
-                const int k = own_end - 1;
+                SHDIAG(SH_POST_S);
+                const int k = lw_own_end(w) - 1;
                 Bd->meta[q][0] = px | (k << 16) | META_SAMPLE;
                 Bd->meta[q][1] = py;
-                own_end = k;
-                sfork = (sfork & ~(0xffu << (8 * k))) | ((uint32_t)q << (8 * k));
-              } else {  // the pending refraction child of the shallowest binary frame
-                const int L = __builtin_ctz(pend);
+                const int sh = 10 + 6 * (k - 1);
+                Bd->lw[threadIdx.x] = (w & ~7u & ~(63u << sh)) | (uint32_t)k | ((uint32_t)q << sh);
+              } else {  // the pending refraction child of frame L, traced at level L + 1
+                SHDIAG(SH_POST_T);
                 const double* e = ext(L);
                 const d3 o = ld3(e, 3), dd = ld3(e, 6);
                 Bd->ray[q][0] = o.x;
@@ -1832,11 +1894,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                 Bd->ray[q][3] = dd.x;
                 Bd->ray[q][4] = dd.y;
                 Bd->ray[q][5] = dd.z;
-                Bd->meta[q][0] = dbase + L + 1;
+                Bd->meta[q][0] = L + 1;
                 Bd->meta[q][1] = 0;
                 const long long pk = __double_as_longlong(core_ld(L, 4));
                 core_st(L, 4, __longlong_as_double(pk | FL_FORKED | ((long long)q << PK_SLOT)));
-                pend &= ~(1u << L);
               }
             }
             if (lane == 0) {
@@ -1849,7 +1910,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       }
       // (c) idle lanes of a drained wave claim posted tasks
       uint64_t il = exhausted ? __ballot(state == S_IDLE) : 0ull;
-      if (il) {
+      if (__builtin_expect(il != 0, 0)) {
         const uint64_t pm0 = __hip_atomic_load(&Bd->post, __ATOMIC_RELAXED, RT_WG_SCOPE);
         const uint64_t pm = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(pm0 >> 32)) << 32) |
                             (uint32_t)__builtin_amdgcn_readfirstlane((int)pm0);
@@ -1863,23 +1924,24 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                                                         __builtin_amdgcn_mbcnt_lo((unsigned int)il, 0u));
           if (state == S_IDLE && rk < (int)__popcll(got)) {
             const int q = nth_bit(got, rk);
+            SHDIAG(SH_CLAIM);
             const int m0 = Bd->meta[q][0];
             if (m0 & META_SAMPLE) {  // sample k of pixel (x, y)
               px = m0 & 0xffff;
               py = Bd->meta[q][1];
               sample = (m0 >> 16) & 3;
-              own_end = sample + 1;
+              Bd->lw[threadIdx.x] = (uint32_t)(sample + 1) | ((uint32_t)(q + 1) << 3);
+              sum = mk(-0.0, -0.0, -0.0);
               rng = sample_rng(px, py, sample);
               need_gen = true;
-              dbase = 0;
-            } else {  // a refraction subtree rooted at level m0
+              sp = 0;
+            } else {  // a refraction subtree at level m0 >= 1, under a sentinel frame
               ray.o = mk(Bd->ray[q][0], Bd->ray[q][1], Bd->ray[q][2]);
               ray.d = mk(Bd->ray[q][3], Bd->ray[q][4], Bd->ray[q][5]);
-              dbase = m0;
+              core_st(m0 - 1, 4, __longlong_as_double((long long)FL_TASK | ((long long)q << PK_SLOT)));
+              Bd->lw[threadIdx.x] = 0u;
+              sp = m0;
             }
-            task = q;
-            sp = 0;
-            pend = 0u;
             state = S_TRACE;
           }
           il = __ballot(state == S_IDLE);
@@ -1896,7 +1958,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if (lane == 0) __hip_atomic_fetch_add(&Bd->nactive, busy ? 1 : -1, __ATOMIC_RELAXED, RT_WG_SCOPE);
         my_active = busy;
       }
-      if (!busy) {
+      if (__builtin_expect(!busy, 0)) {
         // drained (the refill found nothing): wait while the group may still
         // post work; leave once no wave is busy and nothing is posted
         const int na = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&Bd->nactive, __ATOMIC_RELAXED, RT_WG_SCOPE));
@@ -1904,6 +1966,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if ((na == 0 && __builtin_amdgcn_readfirstlane((int)(pm >> 32)) == 0 &&
              __builtin_amdgcn_readfirstlane((int)pm) == 0) ||
             ++spins > RT_SHARE_SPINS) {
+#ifdef RT_PHASE_TIMING
+          if (lane == 0) atomicAdd(P.stats + ST_SHDIAG + SH_SPIN, (unsigned long long)spins);
+#endif
           if (lane == 0 && my_idle) __hip_atomic_fetch_add(&Bd->nidle, -my_idle, __ATOMIC_RELAXED, RT_WG_SCOPE);
           break;
         }
@@ -1911,7 +1976,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         continue;
       }
       spins = 0;
-      if (!__any(state == S_TRACE || state == S_SHADE || resumed)) {  // only waiting (or quad-holding) lanes
+      if (__builtin_expect(!__any(state == S_TRACE || state == S_SHADE || state == S_RESUME), 0)) {  // only waiting (or quad-holding) lanes
         __builtin_amdgcn_s_sleep(RT_SHARE_SLEEP / 4);
         continue;
       }
@@ -1928,7 +1993,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     PH_MARK(0);
 
     // ---- TRACE pass: closestHit over all objects (raytracer.go:469-483) ----
-    if (__any(state == S_TRACE || resumed)) {
+    if (__any(state == S_TRACE || (RT_SHARE && state == S_RESUME))) {
       const bool tr = state == S_TRACE;
       // Prefetch the parent frame: a ray that misses pops it right after
       // this pass, and the load latency hides under the object loop.
@@ -2099,9 +2164,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           res = lerp(mk(G[3], G[4], G[5]), mk(G[6], G[7], G[8]), t);
         }
       }
-      if (RT_SHARE && resumed) res = board_take(Bd, wait_slot());  // (not tracing: pf is false)
-      unwind((tr && !found) || (RT_SHARE && resumed), res, pf, pf_packed, pf_lw, pf_kr);
-      resumed = false;
+      const bool resumed = RT_SHARE && state == S_RESUME;  // a waiting owner's helper delivered
+      if (__builtin_expect(resumed, 0)) res = board_take(Bd, wait_slot());  // (not tracing: pf is false)
+      unwind((tr && !found) || resumed, res, pf, pf_packed, pf_lw, pf_kr);
       PH_MARK(2);
     }
 
@@ -2705,9 +2770,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           kr = r0 + (1 - r0) * go_pow(1 - cost, 5);
           lw = scale(L, 1.0 - T);
         }
-        const int d = P.depth - dbase - sp;  // depth of the current ray
+        const int d = P.depth - sp;  // depth of the current ray
         if (d - 1 > 0 && (hasR || hasT)) {
-          if (RT_SHARE && hasR && hasT) pend |= 1u << sp;  // the refraction child waits: may be posted
           core_st(sp, 0, lw.x);
           core_st(sp, 1, lw.y);
           core_st(sp, 2, lw.z);

@@ -71,6 +71,8 @@ def load_library(path=None):
     l.rt_specialized.restype = i
     l.rt_spec_precompile.argtypes = [i, C.POINTER(i), i, C.POINTER(C.c_double)]
     l.rt_spec_precompile.restype = i
+    l.rt_set_work_sharing.argtypes = [vp, i]
+    l.rt_set_work_sharing.restype = i
     l.rt_set_tile_order.argtypes = [vp, i]
     l.rt_set_tile_order.restype = i
     l.rt_tile_order_info.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
@@ -153,6 +155,11 @@ class RenderContext:
         estimate -- one centre sample per 8x8 tile -- runs at scene setup);
         identical pixels and counters either way. Applies at once."""
         _check(self.lib.rt_set_tile_order(self.handle, int(bool(enable))), "rt_set_tile_order")
+
+    def set_work_sharing(self, enable=True):
+        """Work sharing at the tail of a launch (specialised kernel only;
+        default off; identical pixels and counters). Applies at once."""
+        _check(self.lib.rt_set_work_sharing(self.handle, int(bool(enable))), "rt_set_work_sharing")
 
     def tile_order_info(self):
         """(active, estimate_ms): whether the current scene's launches use a
@@ -256,6 +263,19 @@ class RenderContext:
         self.render_rows_async(y0, y1, out)
         torch.cuda.synchronize(self.device)
         return out.cpu().numpy()
+
+
+def kernel_source_id():
+    """Identifier of the device code (sha256 of the kernel sources, 16 hex
+    digits): stored with committed PMC summaries so that a bench line only
+    quotes counters recorded with the kernel it times."""
+    import hashlib
+    h = hashlib.sha256()
+    root = os.path.dirname(PKG_DIR)
+    for rel in ("include/rt_abi.h", "go-raytracer_amd/csrc/rt_device.h", "go-raytracer_amd/csrc/rt_render.h"):
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def spec_precompile(kinds, features=0, nlights=0):

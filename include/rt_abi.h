@@ -355,6 +355,17 @@ int rt_set_schedule(rt_context *ctx, int mode);
  * staged in LDS or with a BVH only (the estimate of a brute-force search over
  * a large scene would cost too much). Applies to the current scene at once. */
 int rt_set_tile_order(rt_context *ctx, int enable);
+/* Work sharing at the tail of a launch (MI355X-specific; pixels and counters
+ * are identical either way; default off). With enable != 0 the context's
+ * specialised kernel (rt_set_specialize) is compiled with a per-workgroup
+ * board in LDS: once the work queue is drained, a lane still tracing a pixel
+ * posts the samples it has not started and the pending refraction children
+ * of its binary (reflect + refract, raytracer.go:512-556) frames, idle lanes
+ * of any wave of the group trace them, and the owner joins their colours in
+ * the reference's order. Off by default: its code costs every round of the
+ * kernel more than the tail gains on the BASELINE configs.
+ * Applies to the current scene at once. */
+int rt_set_work_sharing(rt_context *ctx, int enable);
 /* Whether the current scene has a tile order, and the estimate's wall time
  * (ms) at scene setup. */
 int rt_tile_order_info(rt_context *ctx, int *active, double *estimate_ms);
@@ -364,13 +375,16 @@ int rt_tile_order_info(rt_context *ctx, int *active, double *estimate_ms);
  * staged in LDS per workgroup; RT_INFO_BVH a BVH over the bounded objects;
  * RT_INFO_CSG CSG composites; RT_INFO_STREAM a large linear scene whose
  * object records are read from global memory in index order (per-wave LDS
- * chunks, or scalar loads in the brute-force kernel); RT_INFO_WAVEFRONT is
- * reserved (never set). */
+ * chunks, or scalar loads in the brute-force kernel); RT_INFO_WAVEFRONT the
+ * scene's kernel shares work across the lanes and waves of a workgroup at
+ * the tail of a launch (rt_set_work_sharing); RT_INFO_ORDERED launches deal
+ * tiles most expensive first (rt_set_tile_order). */
 #define RT_INFO_LDS 1
 #define RT_INFO_BVH 2
 #define RT_INFO_CSG 4
 #define RT_INFO_STREAM 8
 #define RT_INFO_WAVEFRONT 16
+#define RT_INFO_ORDERED 32
 int rt_scene_info(rt_context *ctx, int *flags);
 
 /* Whether the current scene runs a specialised kernel, and the compile time

@@ -38,6 +38,9 @@ CUS, SIMDS_PER_CU, XCDS = 256, 4, 8
 
 def main():
     pat, out = sys.argv[1], sys.argv[2]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from __graft_entry__ import load_package
+    kernel_src = load_package().render.kernel_source_id()  # the device code these counters come from
     kname = sys.argv[3] if len(sys.argv) > 3 else "rt_render"
     agg = collections.defaultdict(list)
     files = sorted(glob.glob(pat))
@@ -70,6 +73,7 @@ def main():
         "issue_util": 4.0 * (a["SQ_INSTS_VALU"] + a["SQ_INSTS_SALU"]) / simd_cyc,
         "fp64_share_of_valu": f64_insts / a["SQ_INSTS_VALU"],
         "source": [os.path.relpath(f) for f in files],
+        "kernel_src": kernel_src,
         "note": "per-launch averages; see scripts/pmc_roofline.py for the definitions",
     }
     with open(out, "w") as f:

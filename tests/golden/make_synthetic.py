@@ -6,7 +6,8 @@ stored as RGB8 PNG plus the oracle's work counters. Test infrastructure:
 re-run after changing a config; the tests check both the oracle and the HIP
 path against these bytes.
 
-    python tests/golden/make_synthetic.py
+    python tests/golden/make_synthetic.py          # reduced-size goldens
+    python tests/golden/make_synthetic.py --full   # full-size strips (minutes)
 """
 import json
 import os
@@ -30,32 +31,47 @@ CASES = {
     "c4csg_128x72": ("c4csg", 128, 72, None),
     "c5_96x60_rows20-40": ("c5", 96, 60, (20, 40)),
 }
+# Full-size strips of configs too costly for the CPU suite to re-render (the
+# oracle's brute-force 100k-sphere search: minutes on 8 threads); the GPU
+# tests compare the HIP path with these committed bytes and counters.
+# C5 as BASELINE.json states it: one 20-row strip (raytracer.go:632-634 strip
+# seeds) of the full 7680-wide, 4320-row frame, 100 000 spheres, depth 8.
+FULL = {
+    "c5_7680x4320_rows2140-2160": ("c5", 7680, 4320, (2140, 2160)),
+}
 
 
-def render(name):
+def render(name, cases=CASES, threads=8):
     from __graft_entry__ import load_package
     import oracle_bind
     pkg = load_package()
-    cfg, w, h, band = CASES[name]
+    cfg, w, h, band = cases[name]
     packed = pkg.scene.convert(pkg.configs.CONFIGS[cfg](width=w, height=h))
     y0, y1 = band if band else (0, h)
-    img, st = oracle_bind.render_rows(packed, y0, y1)
+    img, st = oracle_bind.render_rows(packed, y0, y1, threads=threads)
     return packed, (y0, y1), img, st
 
 
-def main():
+def write(cases, meta_name, threads=8):
     out = os.path.join(HERE, "synthetic")
     os.makedirs(out, exist_ok=True)
     meta = {}
-    for name in CASES:
-        _, (y0, y1), img, st = render(name)
+    for name in cases:
+        _, (y0, y1), img, st = render(name, cases, threads)
         assert (img[..., 3] == 255).all()
         Image.fromarray(np.ascontiguousarray(img[..., :3])).save(os.path.join(out, name + ".png"), optimize=True)
-        meta[name] = {"config": CASES[name][0], "width": CASES[name][1], "height": CASES[name][2],
+        meta[name] = {"config": cases[name][0], "width": cases[name][1], "height": cases[name][2],
                       "rows": [y0, y1], "stats": st.as_dict()}
         print(name, st.total_rays(), "rays", flush=True)
-    with open(os.path.join(out, "counters.json"), "w") as f:
+    with open(os.path.join(out, meta_name), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
+
+
+def main():
+    if "--full" in sys.argv:  # minutes: the 100k-sphere brute-force strip
+        write(FULL, "counters_full.json", threads=os.cpu_count() or 8)
+    else:
+        write(CASES, "counters.json")
 
 
 if __name__ == "__main__":

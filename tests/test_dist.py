@@ -129,8 +129,8 @@ def _weak_worker(rank, world, port, w, h, q):
 
 
 def test_weak_scaling_frame_per_rank():
-    """bench.py default (--scaling weak): every rank renders the whole frame
-    locally; timing is max over ranks, rays summed."""
+    """bench.py --scaling weak (the default is strong): every rank renders the
+    whole frame locally; timing is max over ranks, rays summed."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind

@@ -16,13 +16,17 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def ctxs():
+    """generic kernel; specialised kernel; specialised kernel with work
+    sharing at the tail (rt_set_work_sharing)"""
     import torch
     assert torch.cuda.is_available()
     g = rt.RenderContext(0)
     s = rt.RenderContext(0, specialize=True)
-    yield g, s
-    g.close()
-    s.close()
+    w = rt.RenderContext(0, specialize=True)
+    w.set_work_sharing(True)
+    yield g, s, w
+    for c in (g, s, w):
+        c.close()
 
 
 def render(ctx, packed):
@@ -56,6 +60,10 @@ CASES = {
 def test_tile_order_and_sharing_match_oracle(ctxs, case):
     packed = rt.scene.convert(CASES[case]())
     ref, ost = oracle_bind.render_rows(packed)
+    ctxs[2].set_scene(packed)
+    assert ctxs[2].scene_info() & rt.abi.RT_INFO_WAVEFRONT
+    ctxs[1].set_scene(packed)
+    assert not ctxs[1].scene_info() & rt.abi.RT_INFO_WAVEFRONT
     for c in ctxs:
         try:
             for order in (True, False):
@@ -74,7 +82,7 @@ def test_tile_order_and_sharing_match_oracle(ctxs, case):
 def test_cost_estimate_leaves_counters_alone(ctxs):
     """The scene-setup estimate launch traces rays too; they must not reach
     the frame's counters."""
-    g, _ = ctxs
+    g = ctxs[0]
     packed = rt.scene.convert(rt.configs.c3(width=128, height=72))
     g.read_stats(reset=True)
     g.set_scene(packed)
@@ -93,7 +101,7 @@ def test_interleaved_shares_with_order_match_full_frame(ctxs):
     """Strong-scaling shares (tile rows r, r + N, ...) each get their own
     tile order; gathered, they are the oracle's frame."""
     import torch
-    _, s = ctxs
+    s = ctxs[2]  # with work sharing
     args = rt.configs.c4(width=160, height=96)
     packed = rt.scene.convert(args)
     ref, ost = oracle_bind.render_rows(packed)
@@ -117,7 +125,7 @@ def test_launches_on_alternating_streams(ctxs):
     another stream waits for the previous one, so back-to-back launches on
     different streams render every row."""
     import torch
-    g, _ = ctxs
+    g = ctxs[0]
     packed = rt.scene.convert(rt.configs.c2(width=200, height=120))
     ref, ost = oracle_bind.render_rows(packed)
     g.set_scene(packed)
@@ -131,4 +139,5 @@ def test_launches_on_alternating_streams(ctxs):
         assert_same(o.cpu().numpy(), ref, "launch %d" % k)
     st = g.read_stats(reset=True)
     for key, v in ost.as_dict().items():
-        assert st.as_dict()[key] == 6 * v, key
+        want = [6 * x for x in v] if isinstance(v, (list, tuple)) else 6 * v
+        assert st.as_dict()[key] == want, key
