@@ -161,6 +161,11 @@ enum { LDS_MAX_BYTES = RT_LDS_MAX };
 // PCG jump table entries: (row within the 20-row strip) x (sample 0..3)
 enum { JUMP_ENTRIES = 20 * 4 };
 
+// Cost estimate (Params::est_out): sample 0 of est_pts (1 or 4) pixels per
+// 8x8 tile -- its centre, or the centres of its four 4x4 quarters.
+__device__ __forceinline__ int est_x(int pts, unsigned int k) { return pts == 1 ? TILE / 2 : 2 + 4 * (int)(k & 1u); }
+__device__ __forceinline__ int est_y(int pts, unsigned int k) { return pts == 1 ? TILE / 2 : 2 + 4 * (int)((k >> 1) & 1u); }
+
 struct Params {
   int lds_frames_off;  // byte offset of the LDS frame cores in dynamic LDS
   int lds_levels;      // recursion levels whose frame core lives in LDS (host: LDS left at full occupancy)
@@ -199,10 +204,11 @@ struct Params {
   // Tile order (host: scene-setup cost estimate, most expensive first): the
   // pool's virtual tile v renders tile order[v] of the launch; nullptr = in order
   const unsigned int* order;
-  // Cost-estimate launch (est_out != nullptr): one unit per 8x8 tile of the
-  // frame, its centre pixel's sample 0 traced in full; est_out[tile] counts the
-  // rays traced for it. Serial-sample kernel only; nothing is written to out.
+  // Cost-estimate launch (est_out != nullptr): est_pts units per 8x8 tile of
+  // the frame, each one pixel's sample 0 traced in full; est_out[tile] counts
+  // the rays traced for them. Serial-sample kernel only; nothing is written to out.
   unsigned int* est_out;
+  int est_pts;  // estimate pixels per tile (1 or 4)
 };
 // Per-lane event counters (u64, LDS, fire-and-forget ds_add), reduced once per
 // workgroup at exit: per-wave 64-bit SGPR counters pushed the kernel into
@@ -1776,12 +1782,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                                    : __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
       unsigned int take = min((unsigned int)__popcll(mask), pool_end - pool_next);
-      if (!QD && P.est_out) {  // cost estimate: unit u = the centre pixel of frame tile u
+      if (!QD && P.est_out) {  // cost estimate: unit u = pixel (u mod est_pts) of frame tile u / est_pts
         if (need && rank < take) {
-          const unsigned int u = pool_next + rank;
-          px = min((int)(u % (unsigned)P.tiles_x) * TILE + TILE / 2, P.width - 1);
-          py = min((int)(u / (unsigned)P.tiles_x) * TILE + TILE / 2, P.y1 - 1);
-          pout = u;
+          const unsigned int u = pool_next + rank, t = u / (unsigned)P.est_pts, k = u % (unsigned)P.est_pts;
+          px = min((int)(t % (unsigned)P.tiles_x) * TILE + est_x(P.est_pts, k), P.width - 1);
+          py = min((int)(t / (unsigned)P.tiles_x) * TILE + est_y(P.est_pts, k), P.y1 - 1);
+          pout = t;
           const int ry = py % 20;
           rng = pcg_jump(Pcg{0xDEADULL ^ (uint64_t)px, 0xBEEFULL ^ (uint64_t)(py - ry)}, jrows[ry * 4],
                          jrows[ry * 4 + 1], jrows[ry * 4 + 2], jrows[ry * 4 + 3]);
