@@ -52,6 +52,16 @@
 #include "../../include/rt_abi.h"
 #include "rt_device.h"
 
+// The generic kernels (every scene flavour, every feature, run-time object
+// loops) get 2 waves/SIMD: at 3 (168 VGPRs) they spilled ~175 VGPRs and
+// ~110 SGPRs to scratch, and one build of that spill-heavy code rendered the
+// deep-glass tiles of C4 wrong in the serial-sample schedule while unrelated
+// source changes (an unused branch, the frame prefetch switched off) made it
+// right again -- code no test could trust. The specialised kernels (hipRTC,
+// RT_MIN_WAVES from rt_render.h) fit 3 waves without spilling.
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 2
+#endif
 #include "rt_render.h"
 #include "rt_jit_src.inc"
 
@@ -1591,7 +1601,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // RT_LDS_FULL=n (experiments) also moves the other frame fields (first
   // child's colour, pending refraction ray) of the first n levels to LDS.
   const int level_bytes = WAVES_PER_WG * CORE * 64 * (int)sizeof(double);
-  const int ext_bytes = WAVES_PER_WG * 9 * 64 * (int)sizeof(double);
+  const int ext_bytes = WAVES_PER_WG * EXT_ROWS * 64 * (int)sizeof(double);
   int lds_levels = plan_hit ? pl.lds_levels : 0, lds_full = plan_hit ? pl.lds_full : 0;
   if (!plan_hit && c->lds_per_cu > 0 && c->lds_per_block > 0) {
     const int avail = std::min(c->lds_per_block, c->lds_per_cu / std::min(per_cu, 8)) - shmem;

@@ -113,11 +113,14 @@ enum { GEO = 16, SHD = 32, MAT = 16, LGT = 16, OMAT = 8, GLOB = 16 };
 // the Exp/Log of a fractional Pow) (read where used, so they
 // do not occupy scalar registers across the whole kernel)
 // Frame of one traceRay activation that has children (post-order combine).
-// Global layout: 14 fields, lane-interleaved: Lw[3] cfirst[3] pend_o[3]
-// pend_d[3] kr packed. The CORE fields (Lw, kr, packed) of the first
-// P.lds_levels levels live in LDS instead; cfirst/pending (only used when a
-// material is both reflective and transparent) always live in HBM.
-enum { FRAME_FIELDS = 18, CORE = 5 };  // 14..16 colour, 17 reflectivity: VM materials only
+// Global layout, lane-interleaved rows: Lw[3] ext[6] kr packed colour[3]
+// reflectivity (the last four for VM materials only). ext holds the pending
+// refraction ray (o, d) while the reflection child runs, then -- the ray read
+// -- the reflection child's colour in its first three rows (a glass frame keeps
+// 6 rows, not 9: a third fewer dirty lines written back per frame). The CORE
+// fields (Lw, kr, packed) of the first P.lds_levels levels live in LDS
+// instead, ext of the first P.lds_full levels too; the rest live in HBM.
+enum { FRAME_FIELDS = 15, CORE = 5, EXT_ROWS = 6, FR_EXT = 3, FR_COL = 11, FR_REFL = 14 };
 enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
 // Work queue: pixels per dequeue -- one 8x8 tile, or with pixel quads a 4x4
 // quarter of one (16 quads = one wave's lanes) -- from QHEADS queue heads
@@ -625,11 +628,12 @@ __device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax
 struct WaveStack {
   int* ref;
   uint64_t* mask;
+  // r and m are wave-uniform: every active lane stores the same value, so
+  // the entry is written whichever lanes are active
   __device__ __forceinline__ void push(int& sp, int lane, int r, uint64_t m) {
-    if (lane == 0) {
-      ref[sp] = r;
-      mask[sp] = m;
-    }
+    (void)lane;
+    ref[sp] = r;
+    mask[sp] = m;
     sp++;
   }
 };
@@ -1058,7 +1062,7 @@ __device__ __forceinline__ d3 ld3(const double* f, int field) {
 }
 
 // CORE field c (0..2 Lw, 3 kr, 4 packed) -> global field index.
-__device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ? 12 : 13); }
+__device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ? 9 : 10); }
 
 // Frame flags (packed with the material index): packed = material << PK_MAT |
 // board slot << PK_SLOT | flags. FL_FORKED: the pending refraction child was
@@ -1388,12 +1392,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (level < lds_lv) return lfr[(level * CORE + c) * 64];
     return frame_ptr(stk, level)[core_gfield(c) * 64];
   };
-  // Frame fields 3..11 (first child's colour, pending refraction ray) of
-  // `level`: row j - 3 of the returned pointer (LDS for level < lds_full).
+  // ext rows of `level` (pending refraction ray, then the first child's
+  // colour; LDS for level < lds_full).
   const int lds_full = P.lds_full;
-  double* lext = reinterpret_cast<double*>(smem + P.lds_ext_off) + (size_t)(threadIdx.x >> 6) * (lds_full * 9 * 64) + lane;
+  double* lext = reinterpret_cast<double*>(smem + P.lds_ext_off) + (size_t)(threadIdx.x >> 6) * (lds_full * EXT_ROWS * 64) + lane;
   auto ext = [&](int level) -> double* {
-    return level < lds_full ? lext + (size_t)level * 9 * 64 : frame_ptr(stk, level) + 3 * 64;
+    return level < lds_full ? lext + (size_t)level * EXT_ROWS * 64 : frame_ptr(stk, level) + FR_EXT * 64;
   };
   auto core_st = [&](int level, int c, double v) {
     if (level < lds_lv)
@@ -1624,31 +1628,34 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             state = S_IDLE;
             have_res = false;
           } else if ((fl & FL_HASR) && (fl & FL_HAST) && !(fl & FL_STAGE)) {
-            // reflection child done; trace the pending refraction child
-            st3(ext(sp - 1), 0, res);
+            // reflection child done; trace the pending refraction child.
+            // Its colour takes the pending ray's rows once the ray is read.
+            double* e = ext(sp - 1);
+            const d3 first = res;
+            bool here = true;
             core_st(sp - 1, 4, __longlong_as_double(packed | FL_STAGE));
             if (RT_SHARE && __builtin_expect((fl & FL_FORKED) != 0, 0)) {
               const int q = (int)((packed >> PK_SLOT) & 63);
               if (board_reclaim(Bd, q)) {  // nobody took it: trace it here
                 SHDIAG(SH_RECLAIM);
                 board_free(Bd, q);
-                ray.o = ld3(ext(sp - 1), 3);
-                ray.d = ld3(ext(sp - 1), 6);
-                state = S_TRACE;
-                have_res = false;
               } else if (board_done(Bd, q)) {
+                here = false;
                 res = board_take(Bd, q);  // the next round combines (FL_STAGE set)
               } else {
                 SHDIAG(SH_WAIT);
+                here = false;
                 state = S_WAIT;  // (the slot is found again from the frame: wait_slot)
                 have_res = false;
               }
-            } else {
-              ray.o = ld3(ext(sp - 1), 3);
-              ray.d = ld3(ext(sp - 1), 6);
+            }
+            if (here) {
+              ray.o = ld3(e, 0);
+              ray.d = ld3(e, 3);
               state = S_TRACE;
               have_res = false;
             }
+            st3(e, 0, first);
           } else {
             const double* FM = S.mats + (size_t)(packed >> PK_MAT) * MAT;
             d3 R = mk(0, 0, 0), Tr = mk(0, 0, 0);
@@ -1672,8 +1679,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             d3 fcol;
             double frefl;
             if (spec_feat(SF_VM) && (fl & FL_VMMAT)) {
-              fcol = ld3(f, 14);
-              frefl = f[17 * 64];
+              fcol = ld3(f, FR_COL);
+              frefl = f[FR_REFL * 64];
             } else {
               fcol = mk(FM[0], FM[1], FM[2]);
               frefl = FM[3];
@@ -1893,7 +1900,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               } else {  // the pending refraction child of frame L, traced at level L + 1
                 SHDIAG(SH_POST_T);
                 const double* e = ext(L);
-                const d3 o = ld3(e, 3), dd = ld3(e, 6);
+                const d3 o = ld3(e, 0), dd = ld3(e, 3);
                 Bd->ray[q][0] = o.x;
                 Bd->ray[q][1] = o.y;
                 Bd->ray[q][2] = o.z;
@@ -2139,7 +2146,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
             const int* ni = reinterpret_cast<const int*>(nb + 12);
             const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
-            float t0, t1;
+            float t0 = 0.0f, t1 = 0.0f;  // (set by may_hit_box when it returns true)
             const bool a0 = act && may_hit_box(of, idf, slack, tmax, nb, t0);
             const bool a1 = act && may_hit_box(of, idf, slack, tmax, nb + 6, t1);
             const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
@@ -2625,7 +2632,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           } else {
             const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
             const int* ni = reinterpret_cast<const int*>(nb + 12);
-            float t0, t1;
+            float t0 = 0.0f, t1 = 0.0f;
             const bool a0 = act && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb, t0);
             const bool a1 = act && ni[3] < occ && may_hit_box(sof, sidf, sslack, stmax, nb + 6, t1);
             const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
@@ -2782,14 +2789,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           core_st(sp, 1, lw.y);
           core_st(sp, 2, lw.z);
           if (hasR && hasT) {
-            st3(ext(sp), 3, trr.o);
-            st3(ext(sp), 6, trr.d);
+            st3(ext(sp), 0, trr.o);
+            st3(ext(sp), 3, trr.d);
           }
           core_st(sp, 3, kr);
           if (spec_feat(SF_VM) && mat < 0) {  // the VM record is per lane: keep what the combine needs
             double* f = frame_ptr(stk, sp);
-            st3(f, 14, col);
-            f[17 * 64] = refl;
+            st3(f, FR_COL, col);
+            f[FR_REFL * 64] = refl;
           }
           long long packed = ((long long)(mat < 0 ? 0 : mat) << PK_MAT) | (mat < 0 ? FL_VMMAT : 0) |
                              (tmode ? FL_TMODE : 0) | (hasR ? FL_HASR : 0) | (hasT ? FL_HAST : 0);
