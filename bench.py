@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--rows", default=None, metavar="Y0:Y1",
                    help="render only rows [Y0, Y1) of the full-size frame (one GPU): a full-width row "
                         "band of a config too costly to render whole (brute-force C5 at 7680x4320)")
+    p.add_argument("--companion", choices=["auto", "off"], default="auto",
+                   help="c3: also time c3cone (C3 with the cone) for the line's c3cone field; "
+                        "off in profiling runs, whose counters must come from C3 frames only")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -66,10 +69,10 @@ def pmc_traffic(config):
     --pmc passes (profiles/traffic_<config>.json, scripts/pmc_traffic.py)."""
     path = os.path.join(ROOT, "profiles", "traffic_%s.json" % config)
     if not os.path.exists(path):
-        return None, None
+        return None, None, None
     with open(path) as f:
         d = json.load(f)
-    return d.get("traffic_bytes"), os.path.relpath(path, ROOT)
+    return d.get("traffic_bytes"), os.path.relpath(path, ROOT), d.get("kernel_src")
 
 
 def pmc_executed(key):
@@ -173,7 +176,14 @@ def side_config(pkg, name, dev, specialize, steps=10, warmup=2):
     kavg = sum(a.elapsed_time(b) for a, b in evs) / steps
     flops = pkg.abi.algorithmic_flops(st, len(rargs.lights)) / steps
     ctx.close()
-    return {"workload": "%s: %s" % (name, pkg.configs.WORKLOADS[name]), "value": round(st.total_rays() / dt / 1e6, 2),
+    ex, exsrc = pmc_executed(name)
+    executed = None
+    if ex is not None and ex.get("kernel_src") == pkg.render.kernel_source_id() and kavg > 0:
+        executed = {"executed_frac": round(ex["executed_fp64_flops"] / (kavg * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4),
+                    "issue_util": round(ex["issue_util"], 4), "pmc_source": exsrc}
+    elif ex is not None:
+        executed = {"pmc_stale": exsrc}
+    return {"executed": executed, "workload": "%s: %s" % (name, pkg.configs.WORKLOADS[name]), "value": round(st.total_rays() / dt / 1e6, 2),
             "unit": "Mrays/s", "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms": round(kavg, 4),
             "rays_per_step": int(st.total_rays() / steps),
             "frac": round(flops / (kavg * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4), "parity": "unpinned (cone: contest extension)"}
@@ -319,11 +329,14 @@ def main():
                 "issue_util": round(ex["issue_util"], 4),
                 "lane_util": round(ex["lane_util"], 4),
                 "pmc_source": exsrc})
-        tb, src = pmc_traffic(args.config)
+        tb, src, tsrc = pmc_traffic(args.config)
+        if tb is not None and tsrc != pkg.render.kernel_source_id():
+            line["roofline"]["traffic_stale"] = src  # another kernel build's counters
+            tb = None
         if tb is not None and world == 1 and not args.width and not args.height and not band:
             line["roofline"]["traffic"] = int(tb)
             line["roofline"]["traffic_source"] = src
-        if world == 1 and args.config == "c3" and not (args.width or args.height or band):
+        if world == 1 and args.config == "c3" and args.companion == "auto" and not (args.width or args.height or band):
             line["c3cone"] = side_config(pkg, "c3cone", dev, args.specialize == "on")
         if world == 1 and args.cpu_baseline == "auto":
             line["cpu_baseline"] = cpu_baseline(packed, args.cpu_threads)

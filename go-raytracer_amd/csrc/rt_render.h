@@ -30,6 +30,13 @@
                        // slower -- a skip pays only when the whole wave skips, the tests and
                        // branches are paid always
 #endif
+// Framebuffer stores (raytracer.go:656): a lane holds its finished pixel and
+// the wave stores all held pixels with one instruction when a holder is about
+// to finish another pixel, and at exit -- instead of one store per scheduling
+// round in which some lane finished (0: store at once, A/B).
+#ifndef RT_PIX_BATCH
+#define RT_PIX_BATCH 1
+#endif
 #ifndef RT_FRAME_PREFETCH
 #define RT_FRAME_PREFETCH 1  // load the parent frame during the TRACE pass
 #endif
@@ -1480,6 +1487,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   bool need_gen = false;  // lane waits for its next sample ray
   int px = 0, py = 0, sample = 0, sp = 0;
   unsigned int pout = 0;  // output pixel index
+  // Finished pixel held for the wave's next batched framebuffer store
+  // (RT_PIX_BATCH): index (~0u = none) and RGBA8 value.
+  uint32_t held_px = ~0u, held_val = 0u;
+  // One store instruction for every lane's held pixel (wave-uniform call).
+  auto flush_pixels = [&]() {
+    if (held_px != ~0u) P.out[held_px] = held_val;
+    held_px = ~0u;
+  };
   // work sharing (RT_SHARE): per-lane sample bookkeeping in Bd->lw (Board)
   const int wave = (int)(threadIdx.x >> 6);
   int my_idle = 0, spins = 0;  // wave-uniform: idle lanes this wave reports, idle rounds
@@ -1565,7 +1580,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         P.out[pout] = lane_cost;
         lane_cost = 0;
 #else
-        P.out[pout] = (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+        const uint32_t v = (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+        if (RT_PIX_BATCH) {  // (the S_ADV block flushed a previously held pixel)
+          held_px = pout;
+          held_val = v;
+        } else {
+          P.out[pout] = v;
+        }
 #endif
         state = S_IDLE;
         return;
@@ -1711,6 +1732,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     // one (or hands a claimed sample's colour to its owner) ----
     if constexpr (!QD) {
       if (__any(state == S_ADV)) {
+        // a lane about to finish a pixel while it still holds one: every
+        // held pixel goes out in one store first (with sharing a lane may also
+        // finish by taking helpers' colours, so any advancing holder flushes)
+        if (RT_PIX_BATCH && __any(state == S_ADV && held_px != ~0u && (RT_SHARE || sample == 4))) flush_pixels();
         if (state == S_ADV) {
           const uint32_t w = RT_SHARE ? Bd->lw[threadIdx.x] : 4u;
           if (RT_SHARE && __builtin_expect(lw_task(w) >= 0, 0)) {
@@ -1737,12 +1762,19 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const int lk = (lane + k) & 63;
           sm = add(sm, mk(__shfl(sum.x, lk), __shfl(sum.y, lk), __shfl(sum.z, lk)));
         }
+        if (RT_PIX_BATCH && __any(((qd >> lane) & 1) && held_px != ~0u)) flush_pixels();
         if ((qd >> lane) & 1) {
           const d3 c = scale(sm, 1.0 / 4.0);
           const uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
           const uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
           const uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
-          P.out[pout] = (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+          const uint32_t v = (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+          if (RT_PIX_BATCH) {
+            held_px = pout;
+            held_val = v;
+          } else {
+            P.out[pout] = v;
+          }
         }
         if ((qd >> (lane & ~3)) & 1) state = S_IDLE;
       }
@@ -2185,7 +2217,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 
     // ---- SHADE pass, once enough lanes hold a hit ----
     const uint64_t nsh = popc_ballot(state == S_SHADE);
-    const uint64_t ntr = popc_ballot(state == S_TRACE);
+    // (a lane that finished a sample and starts the next one at the loop top,
+    // S_ADV, counts as tracing: leaving it out ran SHADE with fewer lanes,
+    // lane utilisation 0.83 -> 0.74 and C3 +5 %)
+    const uint64_t ntr = popc_ballot(state == S_TRACE || (!QD && state == S_ADV && (RT_SHARE || sample < 4)));
     if (nsh == 0 || (ntr != 0 && nsh * RT_SHADE_DEN < (nsh + ntr) * RT_SHADE_NUM)) continue;
 
     const bool hit = state == S_SHADE;
@@ -2814,6 +2849,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     unwind(have_res, res, false, 0, mk(0, 0, 0), 0.0);
     PH_MARK(7);
   }
+  if (RT_PIX_BATCH) flush_pixels();
 
   if (lane == 0) {
 #ifdef RT_PHASE_TIMING

@@ -1,0 +1,10 @@
+# PMC passes (scripts/gpu_pmc.sh) for every BASELINE config the bench quotes:
+# profiles/pmc_<cfg>.json (executed FP64 work, issue / lane utilisation) and
+# profiles/traffic_<cfg>.json (calibrated HBM bytes) land under gpurun_out/pmc_<cfg>/.
+# usage: bash scripts/gpu_pmc_all.sh "c3 c3cone c4 c4csg c5"
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+for c in ${1:-c3 c3cone c4 c4csg c5}; do
+  bash scripts/gpu_pmc.sh $c > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 gpurun_out/pmc_$c.log; exit 1; }
+  echo "== $c"; tail -2 gpurun_out/pmc_$c.log
+done

@@ -10,7 +10,7 @@ timeout -k 10 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/cal_f -o cal_f
 timeout -k 10 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/cal_w -o cal_w --output-format csv -- ./build_variants/pmc_calib > /dev/null 2>&1 || { echo "calibration failed"; exit 1; }
 for v in ${1:-0 1 2}; do
   export RT_LDS_FULL=$v RT_DEBUG_LAUNCH=1
-  B="python3 bench.py --config c3 --steps 10 --warmup 2 --cpu-baseline off"
+  B="python3 bench.py --config c3 --steps 10 --warmup 2 --cpu-baseline off --companion off"
   timeout -k 10 200 $B > $O/b$v.json 2> $O/b$v.err || { echo "bench $v failed"; tail -3 $O/b$v.err; exit 1; }
   timeout -k 10 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/f$v -o f --output-format csv -- $B > /dev/null 2>&1 && \
   timeout -k 10 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/w$v -o w --output-format csv -- $B > /dev/null 2>&1 || { echo "pmc $v failed"; exit 1; }

@@ -39,15 +39,14 @@ CUS, SIMDS_PER_CU, XCDS = 256, 4, 8
 def main():
     pat, out = sys.argv[1], sys.argv[2]
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from __graft_entry__ import load_package
     kernel_src = load_package().render.kernel_source_id()  # the device code these counters come from
     kname = sys.argv[3] if len(sys.argv) > 3 else "rt_render"
-    agg = collections.defaultdict(list)
     files = sorted(glob.glob(pat))
-    for f in files:
-        for r in csv.DictReader(open(f)):
-            if kname in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    from pmc_common import frame_counters, kept_dispatches
+    agg = frame_counters(pat, kname)  # frame launches only (no estimate / companion)
+    kept, dropped = kept_dispatches(pat, kname)
     a = {k: sum(v) / len(v) for k, v in agg.items()}
     need = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
             "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE"]
@@ -74,6 +73,7 @@ def main():
         "fp64_share_of_valu": f64_insts / a["SQ_INSTS_VALU"],
         "source": [os.path.relpath(f) for f in files],
         "kernel_src": kernel_src,
+        "dispatches_dropped": dropped,
         "note": "per-launch averages; see scripts/pmc_roofline.py for the definitions",
     }
     with open(out, "w") as f:

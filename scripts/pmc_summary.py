@@ -1,16 +1,14 @@
-"""Summarise rocprofv3 --pmc CSVs for one kernel (average per dispatch)."""
-import collections
-import csv
-import glob
+"""Summarise rocprofv3 --pmc CSVs for one kernel (average per frame
+dispatch; the tile-cost estimate launch is left out, see pmc_common.py)."""
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_common import frame_counters  # noqa: E402
 
 pat = sys.argv[1]
 kname = sys.argv[2] if len(sys.argv) > 2 else "rt_render"
-agg = collections.defaultdict(list)
-for f in glob.glob(pat):
-    for r in csv.DictReader(open(f)):
-        if kname in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+agg = frame_counters(pat, kname)
 for k in sorted(agg):
     v = agg[k]
     print("%-28s n=%d avg=%.4g" % (k, len(v), sum(v) / len(v)))

@@ -17,6 +17,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 CAL_BYTES = 512 << 20  # bytes each calibration kernel moves
@@ -31,10 +32,12 @@ def collect(pattern, match):
     return agg
 
 
-render = collect(sys.argv[1], lambda k: "rt_render" in k)
-a = collections.defaultdict(list)
-for (_, c), v in render.items():
-    a[c].extend(v)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pmc_common import frame_counters, kept_dispatches  # noqa: E402
+from __graft_entry__ import load_package  # noqa: E402
+
+a = frame_counters(sys.argv[1])  # frame launches only (no estimate / companion)
 avg = {c: sum(v) / len(v) for c, v in a.items()}
 raw_fetch = avg.get("FETCH_SIZE", 0.0) * 1024.0
 raw_write = avg.get("WRITE_SIZE", 0.0) * 1024.0
@@ -42,6 +45,8 @@ out = {
     "raw_fetch_bytes": raw_fetch,
     "raw_write_bytes": raw_write,
     "dispatches": {c: len(v) for c, v in a.items()},
+    "dispatches_dropped": kept_dispatches(sys.argv[1])[1],
+    "kernel_src": load_package().render.kernel_source_id(),  # the device code these counters come from
 }
 cal = {}
 if len(sys.argv) > 3:
