@@ -710,12 +710,14 @@ void csg_mask_program(const int* code, int len, std::vector<int>& out) {
 // recursion depth >= 7 (C4, C5, canned, c4csg: the glass trees of the last
 // pixels otherwise keep a few waves running long after the rest), and scenes
 // with branching materials (reflective and transparent: binary ray trees)
-// when a launch gives each lane fewer than 32 pixels -- a strong-scaling
-// share of a frame (C3 over 2 / 4 / 8 ranks: 2.37 / 1.78 / 1.40 ms serial vs
-// 2.11 / 1.07 / 0.64 ms with quads) -- and any scene below 4 pixels per lane
-// (C2 over 4 / 8 ranks: 0.22 / 0.19 vs 0.18 / 0.14 ms). Otherwise the idle
-// siblings cost more than the balance gains (C3 whole frame 3.67 vs 4.30 ms,
-// C2 0.38 vs 0.45 ms).
+// when a launch gives each lane fewer than 16 pixels -- a strong-scaling
+// share of a frame (C3 over 4 / 8 ranks: 1.65 / 1.63 ms serial vs 0.99 /
+// 0.55 ms with quads: serially a deep glass pixel's 4 samples alone take
+// ~1.6 ms; over 2 ranks, 21 pixels per lane, serial wins: 1.98 vs 2.10 ms,
+// c3cone 2.26 vs 2.22, profiles/r03/strong) -- and any scene below 4 pixels
+// per lane (C2 over 4 / 8 ranks: 0.22 / 0.19 vs 0.18 / 0.14 ms). Otherwise the
+// idle siblings cost more than the balance gains (C3 whole frame 3.44 vs
+// 4.39 ms, C2 0.38 vs 0.45 ms).
 // rt_set_schedule overrides the choice; so does RT_PIXEL_QUADS=0/1 in the
 // environment at process start (experiments).
 bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus) {
@@ -724,7 +726,7 @@ bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus) {
   if (sched == RT_SCHED_PIXEL) return false;
   if (sched == RT_SCHED_QUADS) return true;
   const double lanes = (double)std::max(1, cus) * 4 * 3 * 64;  // 3 waves per SIMD
-  return s.depth >= 7 || (double)pixels < (s.branching ? 32.0 : 4.0) * lanes;
+  return s.depth >= 7 || (double)pixels < (s.branching ? 16.0 : 4.0) * lanes;
 }
 
 bool scene_in_lds(const DevScene& s) {
@@ -1523,13 +1525,22 @@ static int order_for(rt_context* c, int y0, int trow0, int stride, int tiles_x, 
   // order, measured no better (profiles/r03/order). RT_ORDER_TOP=d
   // (environment, experiments): the costliest 1/d first, d = 1 sorts all.
   static const int topd = getenv("RT_ORDER_TOP") ? std::max(1, atoi(getenv("RT_ORDER_TOP"))) : 4;
+  // RT_ORDER_TAIL=d (experiments): the cheapest 1/d of the tiles go last, in
+  // tile order, so waves that run out of work early finish on short tiles.
+  // Measured slower: C3 3.53-3.56 vs 3.43 ms, C4 5.25-5.29 vs 5.16 (d = 4, 8,
+  // 16), 8-rank shares within 2 % (profiles/r03/order/tail.log): off.
+  static const int taild = getenv("RT_ORDER_TAIL") ? std::max(0, atoi(getenv("RT_ORDER_TAIL"))) : 0;
   {
     const int top = n / topd;
-    std::vector<char> in_top(n, 0);
-    for (int i = 0; i < top; i++) in_top[ord[i]] = 1;
+    const int tail = taild > 0 ? std::min(n - top, n / taild) : 0;
+    std::vector<char> cls(n, 1);  // 0 costliest (first, cost order), 1 middle, 2 cheapest (last)
+    for (int i = 0; i < top; i++) cls[ord[i]] = 0;
+    for (int i = n - tail; i < n; i++) cls[ord[i]] = 2;
     int k = top;
     for (int v = 0; v < n; v++)
-      if (!in_top[v]) ord[k++] = (uint32_t)v;
+      if (cls[v] == 1) ord[k++] = (uint32_t)v;
+    for (int v = 0; v < n; v++)
+      if (cls[v] == 2) ord[k++] = (uint32_t)v;
   }
   unsigned int* d = nullptr;
   HIP_TRY(hipMalloc((void**)&d, (size_t)n * sizeof(unsigned int)));

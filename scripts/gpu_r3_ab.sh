@@ -15,9 +15,10 @@ for c in $CFGS; do
     envs=""; flags="$f"
     case "$f" in *"|"*) envs="${f%%|*}"; flags="${f#*|}";; esac
     [ "$flags" = "-" ] && flags=""
+    [ "$envs" = "-" ] && envs=""
     steps=20; [ $c = c4csg ] && steps=6; [ $c = c5 ] && steps=3
     if [ -n "$flags" ]; then export RT_SPEC_EXTRA_FLAGS="$flags"; else unset RT_SPEC_EXTRA_FLAGS; fi
-    env $envs timeout -k 10 300 python bench.py --config $c --steps $steps --warmup 2 --cpu-baseline off > $O/$c-$tag-$round.json 2> $O/$c-$tag-$round.err || { tail -5 $O/$c-$tag-$round.err; exit 1; }
+    env $envs timeout -k 10 300 python bench.py --config $c --steps $steps --warmup 2 --cpu-baseline off --companion off > $O/$c-$tag-$round.json 2> $O/$c-$tag-$round.err || { tail -5 $O/$c-$tag-$round.err; exit 1; }
     echo "r$round $c [$f] $(python3 -c "import json; d=json.load(open('$O/$c-$tag-$round.json')); print(d['ms_per_step'], d['roofline']['kernel_ms'], d['config'].get('tile_order_ms'))")"
   done
 done

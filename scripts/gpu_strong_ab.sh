@@ -12,6 +12,7 @@ for c in $CFGS; do
     envs=""; flags="$f"
     case "$f" in *"|"*) envs="${f%%|*}"; flags="${f#*|}";; esac
     [ "$flags" = "-" ] && flags=""
+    [ "$envs" = "-" ] && envs=""
     if [ -n "$flags" ]; then export RT_SPEC_EXTRA_FLAGS="$flags"; else unset RT_SPEC_EXTRA_FLAGS; fi
     env $envs STRONG_WORLDS=${STRONG_WORLDS:-1,8} timeout -k 10 300 python3 scripts/strong_emul.py $c 10 > $O/$c-$tag.json 2> $O/$c-$tag.err || { tail -5 $O/$c-$tag.err; exit 1; }
     echo "$c [$f] $(cat $O/$c-$tag.json)"

@@ -3,7 +3,8 @@ frame (interleaved 8-row tile rows, stride = world) for world = 1, 2, 4, 8, as
 bench.py --scaling strong would launch it on each rank (no collective here).
 efficiency(world) = t(1) / (world * t(world)); with STRONG_ALL_RANKS=1 (default)
 every rank's share is timed too and w<N>_eff_max uses the slowest one.
-usage: python scripts/strong_emul.py [config] [steps]   (STRONG_WORLDS=1,2,4,8 by default)"""
+usage: python scripts/strong_emul.py [config] [steps]   (STRONG_WORLDS=1,2,4,8 by default;
+STRONG_SHARING=1: the context compiled with work sharing)"""
 import json
 import os
 import sys
@@ -22,6 +23,8 @@ def main():
     torch.cuda.set_device(0)
     packed = pkg.scene.convert(pkg.configs.CONFIGS[cfg]())
     ctx = pkg.RenderContext(0, specialize=True)
+    if os.environ.get("STRONG_SHARING") == "1":  # work sharing at the tail (rt_set_work_sharing)
+        ctx.set_work_sharing(True)
     ctx.set_scene(packed)
     out = {"config": cfg}
     t1 = None
