@@ -220,6 +220,8 @@ def main():
     spec_active, spec_ms = ctx.specialized()
     order_active, order_ms = ctx.tile_order_info()
     bvh = bool(ctx.scene_info() & pkg.abi.RT_INFO_BVH)
+    # CSG composites are an extension: the reference has no flop model for them
+    no_ref_model = bool(ctx.scene_info() & pkg.abi.RT_INFO_CSG)
     mode = "frame" if args.scaling == "weak" else args.shard
     band = None
     if args.rows:
@@ -303,9 +305,9 @@ def main():
                          # Intersect calls, so reference work per second is no
                          # utilisation (it can exceed 1): null, and the executed
                          # fraction (PMC) carries the roofline instead
-                         "frac": None if bvh else round(achieved_tf / PEAK_FP64_TFLOPS, 4),
+                         "frac": None if (bvh or no_ref_model) else round(achieved_tf / PEAK_FP64_TFLOPS, 4),
                          "reference_work_frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
-                         "frac_nofma_ceiling": None if bvh else round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),
+                         "frac_nofma_ceiling": None if (bvh or no_ref_model) else round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),
                          "kernel_ms": round(kavg, 4), "flops_per_launch": int(flops_per_launch),
                          "hbm_out_gbs": round(out_bytes / (kavg * 1e-3) / 1e9, 2) if kavg > 0 else None,
                          "traffic": None, "traffic_source": None},
