@@ -14,7 +14,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("name", ["pmc_c3", "pmc_c5_bf_rows2048-2304"])
+@pytest.mark.parametrize("name", ["pmc_c3", "pmc_c3cone", "pmc_c4", "pmc_c4csg", "pmc_c5", "pmc_c5_bf_rows2048-2304"])
 def test_pmc_summary_recomputes_from_committed_csvs(tmp_path, name):
     ref = json.load(open(os.path.join(ROOT, "profiles", name + ".json")))
     srcs = [os.path.join(ROOT, f) for f in ref["source"]]
