@@ -485,6 +485,8 @@ struct rt_context {
   unsigned int* queue = nullptr;  // two sets of QHEADS queue heads (launches alternate)
   int qset = 0;                    // the set the next launch dequeues from
   unsigned long long* stats = nullptr;
+  unsigned long long* stats_part = nullptr;  // [workgroup slot][STATS_PART] frame counters (Params::stats_part)
+  int stats_parts = 0;                       // workgroup slots (cus * 8: any persistent grid)
   double* stack = nullptr;
   double* vm_global = nullptr;  // per-lane VM material records (global flavour)
   size_t vm_global_bytes = 0;
@@ -1013,6 +1015,11 @@ int rt_create(int device, rt_context** out) {
     rc = fail(RT_E_NOMEM, "stats alloc");
   if (rc == RT_OK && hipMemset(c->stats, 0, sizeof(unsigned long long) * 64) != hipSuccess)
     rc = fail(RT_E_DEVICE, "stats memset");
+  c->stats_parts = c->cus * 8;
+  if (rc == RT_OK && hipMalloc((void**)&c->stats_part, sizeof(unsigned long long) * STATS_PART * c->stats_parts) != hipSuccess)
+    rc = fail(RT_E_NOMEM, "stats alloc");
+  if (rc == RT_OK && hipMemset(c->stats_part, 0, sizeof(unsigned long long) * STATS_PART * c->stats_parts) != hipSuccess)
+    rc = fail(RT_E_DEVICE, "stats memset");
   if (rc == RT_OK && (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess))
     rc = fail(RT_E_DEVICE, "event create");
   if (rc != RT_OK) {
@@ -1031,6 +1038,7 @@ void rt_destroy(rt_context* c) {
   (void)hipFree(c->jump);
   (void)hipFree(c->queue);
   (void)hipFree(c->stats);
+  (void)hipFree(c->stats_part);
   (void)hipFree(c->stack);
   (void)hipFree(c->vm_global);
   clear_orders(c);
@@ -1666,6 +1674,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.queue = c->queue + c->qset * QSET;
   P.queue_next = c->queue + (1 - c->qset) * QSET;
   P.stats = est ? c->est_stats : c->stats;
+  P.stats_part = est ? nullptr : c->stats_part;  // the estimate's counts are not the frame's
   P.est_out = est ? c->est : nullptr;
 #ifdef RT_PHASE_TIMING
   if (!c->wdiag && hipMalloc((void**)&c->wdiag, sizeof(unsigned long long) * 4 * 8192) != hipSuccess) c->wdiag = nullptr;
@@ -1742,14 +1751,16 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   return RT_OK;
 }
 
-// Which scenes get a tile order: the estimate traces one sample per 8x8 tile
-// (1/256 of the frame's samples) -- cheap for scenes in LDS or with a BVH, not
-// for the brute-force search over a large scene. RT_TILE_ORDER=0 (environment,
-// experiments) turns it off.
+// Which scenes get a tile order: scenes in LDS (C2, C3, C4's BVH, c4csg).
+// Scenes read from HBM lose by it: the BVH of C5 (100 k spheres) runs from the
+// L2, and tiles dealt out of neighbourhood order thrash it (C5 517-527 vs
+// 459-479 ms unordered); the brute-force search over a large scene would pay
+// a costly estimate. RT_TILE_ORDER=0 / 2 (environment, experiments): never /
+// also for HBM scenes with a BVH.
 static bool want_order(const rt_context* c) {
   static const int env = getenv("RT_TILE_ORDER") ? atoi(getenv("RT_TILE_ORDER")) : 1;
   const DevScene& s = c->sc;
-  return env != 0 && c->order_on && s.nobj > 0 && (scene_in_lds(s) || s.use_bvh);
+  return env != 0 && c->order_on && s.nobj > 0 && (scene_in_lds(s) || (env == 2 && s.use_bvh));
 }
 
 // Scene setup: the estimate launch (one centre sample per frame tile, traced
@@ -1830,14 +1841,19 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
   if (!c || !out) return fail(RT_E_INVALID, "rt_read_stats: NULL argument");
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
-  unsigned long long h[ST_COUNT], wd = 0;
-  HIP_TRY(hipMemcpyAsync(h, c->stats, sizeof h, hipMemcpyDeviceToHost, st));
+  unsigned long long h[ST_COUNT] = {}, wd = 0;
+  // frame counters: one record per workgroup slot, summed here
+  std::vector<unsigned long long> part((size_t)STATS_PART * c->stats_parts);
+  HIP_TRY(hipMemcpyAsync(part.data(), c->stats_part, part.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(&wd, c->stats + ST_WATCHDOG, sizeof wd, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  for (int b = 0; b < c->stats_parts; b++)
+    for (int k = 0; k < ST_COUNT; k++) h[k] += part[(size_t)b * STATS_PART + k];
   if (wd) {
     // the frames since the last reset are incomplete: clear everything (as a
     // reset would) so that later reads report later launches, then fail
     HIP_TRY(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st));
+    HIP_TRY(hipMemsetAsync(c->stats_part, 0, part.size() * sizeof(unsigned long long), st));
     HIP_TRY(hipStreamSynchronize(st));
     c->primary_pending = 0;
     c->launches = 0;
@@ -1926,6 +1942,7 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
   if (c->timed && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) out->kernel_ms = ms;
   if (reset) {
     HIP_TRY(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st));
+    HIP_TRY(hipMemsetAsync(c->stats_part, 0, part.size() * sizeof(unsigned long long), st));
     HIP_TRY(hipStreamSynchronize(st));
     c->primary_pending = 0;
     c->launches = 0;

@@ -347,13 +347,15 @@ int rt_set_accel(rt_context *ctx, int flags);
 int rt_set_schedule(rt_context *ctx, int mode);
 
 /* Tile order (MI355X-specific; pixels and counters are identical either
- * way). With enable != 0 (default) rt_set_scene also traces one centre sample
- * per 8x8 tile of the frame at full depth and counts its rays; every launch
- * then deals its tiles most expensive first (longest-processing-time-first),
- * so the end of a launch is made of cheap tiles instead of the deep glass
- * trees that otherwise keep a few waves running long after the rest. Scenes
- * staged in LDS or with a BVH only (the estimate of a brute-force search over
- * a large scene would cost too much). Applies to the current scene at once. */
+ * way). With enable != 0 (default) rt_set_scene also traces sample 0 of four
+ * pixels per 8x8 tile of the frame at full depth and counts its rays (none of
+ * them reach rt_read_stats); every launch then deals the costliest quarter of
+ * its tiles first, in cost order, and the rest in tile order, so the deep
+ * glass trees start early instead of keeping a few waves running after the
+ * rest, while most tiles keep their neighbours' locality. Scenes staged in
+ * LDS only: a scene read from HBM (a large BVH) loses more cache locality
+ * than it gains. Applies to the current scene at once; rt_tile_order_info
+ * reports whether an order is active and the estimate's wall time. */
 int rt_set_tile_order(rt_context *ctx, int enable);
 /* Work sharing at the tail of a launch (MI355X-specific; pixels and counters
  * are identical either way; default off). With enable != 0 the context's
