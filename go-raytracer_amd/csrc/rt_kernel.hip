@@ -1007,9 +1007,9 @@ int rt_create(int device, rt_context** out) {
     }
   }
   int rc = upload(&c->jump, jump);
-  if (rc == RT_OK && hipMalloc((void**)&c->queue, 2 * QSET * sizeof(unsigned int)) != hipSuccess)
+  if (rc == RT_OK && hipMalloc((void**)&c->queue, 2 * QSET_ALLOC * sizeof(unsigned int)) != hipSuccess)
     rc = fail(RT_E_NOMEM, "queue alloc");
-  if (rc == RT_OK && hipMemset(c->queue, 0, 2 * QSET * sizeof(unsigned int)) != hipSuccess)
+  if (rc == RT_OK && hipMemset(c->queue, 0, 2 * QSET_ALLOC * sizeof(unsigned int)) != hipSuccess)
     rc = fail(RT_E_DEVICE, "queue memset");
   if (rc == RT_OK && hipMalloc((void**)&c->stats, sizeof(unsigned long long) * 64) != hipSuccess)
     rc = fail(RT_E_NOMEM, "stats alloc");
@@ -1671,8 +1671,8 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.jump = c->jump;
   // this launch dequeues from set qset and zeroes the other set for the next
   // one (launches on a context are stream-ordered): no memset per launch
-  P.queue = c->queue + c->qset * QSET;
-  P.queue_next = c->queue + (1 - c->qset) * QSET;
+  P.queue = c->queue + c->qset * QSET_ALLOC;
+  P.queue_next = c->queue + (1 - c->qset) * QSET_ALLOC;
   P.stats = est ? c->est_stats : c->stats;
   P.stats_part = est ? nullptr : c->stats_part;  // the estimate's counts are not the frame's
   P.est_out = est ? c->est : nullptr;

@@ -134,7 +134,11 @@ enum { CHUNK = 64, TILE = 8, WG = 256, WAVES_PER_WG = WG / 64 };
 // (chunk c belongs to head c mod QHEADS; a workgroup dequeues from head
 // blockIdx mod QHEADS, see RT_QSTEAL), so the dequeue rate
 // stays below what one atomic word sustains.
-enum { QHEADS = 8, QSTRIDE = 16 /* u32 between heads: 64 B */ };
+#ifndef RT_QHEADS
+#define RT_QHEADS 8
+#endif
+enum { QHEADS = RT_QHEADS /* <= 32: the drained-head mask is 32 bits */, QSTRIDE = 16 /* u32 between heads: 64 B */ };
+static_assert(RT_QHEADS >= 1 && RT_QHEADS <= 32, "RT_QHEADS");
 // Heads a workgroup dequeues from: its home head, then RT_QSTEAL others once
 // that is drained. Every head is drained by its home workgroups, so stopping
 // early never drops a chunk; it bounds the end-of-launch probes (each a
@@ -147,7 +151,8 @@ enum { QHEADS = 8, QSTRIDE = 16 /* u32 between heads: 64 B */ };
 #ifndef RT_QSTEAL
 #define RT_QSTEAL 1
 #endif
-enum { QSET = QHEADS * QSTRIDE /* u32 per launch set of heads */ };
+enum { QSET = QHEADS * QSTRIDE /* u32 per launch set of heads */,
+       QSET_ALLOC = 32 * QSTRIDE /* host: room for any RT_QHEADS build */ };
 #ifndef RT_QCHUNK_PIXEL
 #define RT_QCHUNK_PIXEL 64  // pixels per dequeue without quads (a multiple of 16 dividing 64)
 #endif
