@@ -10,6 +10,14 @@ batch of N frames, one per GPU, with no data-path collective. One process per
 GPU. Workload = config C3 (3840x2160, depth 6, cylinder + cube +
 sphere-for-cone, 4 lights).
 
+Frames in flight (--inflight F, default 2): each rank holds F render contexts
+with the scene and launches consecutive steps on them round-robin, one stream
+each, so the next frame's workgroups take the CUs the current frame's last
+waves leave idle. Each step still renders its whole frame (or share) into its
+own buffer; kernel_ms (the roofline's time) is then the GPU span per frame, not
+one launch's start-to-end duration, which overlaps its neighbours
+(roofline.launch_ms_overlapped).
+
 Rays = primary + secondary + shadow, counted on the device with the same rule
 as the CPU oracle (include/rt_abi.h rt_stats). value = rays of all ranks per
 step / max-over-ranks step time.
@@ -58,6 +66,10 @@ def parse():
     p.add_argument("--companion", choices=["auto", "off"], default="auto",
                    help="c3: also time c3cone (C3 with the cone) for the line's c3cone field; "
                         "off in profiling runs, whose counters must come from C3 frames only")
+    p.add_argument("--inflight", type=int, default=2,
+                   help="frames in flight per rank: F render contexts with the same scene on F streams "
+                        "render consecutive frames round-robin, so one frame's tail overlaps the next "
+                        "frame's head (every frame still rendered whole; 1 = serial launches)")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -150,32 +162,54 @@ def cpu_baseline(packed, threads, budget_s=10.0):
     return out
 
 
-def side_config(pkg, name, dev, specialize, steps=10, warmup=2):
+def gpu_span_ms(evs):
+    """GPU time per frame over a timed run: first launch's start event to the
+    latest end event, divided by the frame count (HIP events on the launch
+    streams). With frames in flight, launches overlap, so this -- not the
+    average start-to-end duration of one launch -- is the kernel time a
+    frame costs."""
+    span = max(evs[0][0].elapsed_time(e1) for _, e1 in evs)
+    return span / len(evs)
+
+
+def make_contexts(pkg, dev, packed, n, specialize, accel=None):
+    ctxs = []
+    for _ in range(n):
+        c = pkg.RenderContext(dev.index, specialize=specialize)
+        if accel is not None:
+            c.set_accel(accel)
+        c.set_scene(packed)
+        ctxs.append(c)
+    return ctxs
+
+
+def side_config(pkg, name, dev, specialize, inflight, steps=10, warmup=2):
     """One GPU, whole frames of another config (the C3 line's companion: C3 as
-    BASELINE.json states it, with the cone the reference lacks): value,
-    ms/frame and the reference-work roofline fraction."""
+    BASELINE.json states it, with the cone the reference lacks), with the same
+    frames in flight as the main line: value, ms/frame and the reference-work
+    roofline fraction."""
     import torch
     rargs = pkg.configs.CONFIGS[name]()
     packed = pkg.scene.convert(rargs)
-    ctx = pkg.RenderContext(dev.index, specialize=specialize)
-    ctx.set_scene(packed)
-    buf = torch.zeros((packed.height, packed.width, 4), dtype=torch.uint8, device=dev)
-    for _ in range(warmup):
-        ctx.render_rows_async(0, packed.height, buf)
+    ctxs = make_contexts(pkg, dev, packed, inflight, specialize)
+    dr = pkg.dist.DistributedRenderer(ctxs, packed, 0, 1, dev, mode="frame")
+    for _ in range(max(warmup, inflight)):
+        dr.step()
+    dr.flush()
     torch.cuda.synchronize()
-    ctx.read_stats(reset=True)
+    dr.read_stats(reset=True)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record()
-        ctx.render_rows_async(0, packed.height, buf)
-        e1.record()
+    for k in range(steps):
+        dr.step(events=evs[k])
+    dr.flush()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    st = ctx.read_stats(reset=True)
-    kavg = sum(a.elapsed_time(b) for a, b in evs) / steps
+    st = dr.read_stats(reset=True)
+    kavg = gpu_span_ms(evs)
     flops = pkg.abi.algorithmic_flops(st, len(rargs.lights)) / steps
-    ctx.close()
+    for c in ctxs:
+        c.close()
     ex, exsrc = pmc_executed(name)
     executed = None
     if ex is not None and ex.get("kernel_src") == pkg.render.kernel_source_id() and kavg > 0:
@@ -213,10 +247,11 @@ def main():
         kw["height"] = args.height
     rargs = cfg(**kw)
     packed = pkg.scene.convert(rargs)
-    ctx = pkg.RenderContext(local, specialize=args.specialize == "on")
-    if args.accel == "none":
-        ctx.set_accel(0)
-    ctx.set_scene(packed)
+    if args.inflight < 1:
+        raise SystemExit("--inflight must be >= 1")
+    ctxs = make_contexts(pkg, dev, packed, args.inflight, args.specialize == "on",
+                         accel=0 if args.accel == "none" else None)
+    ctx = ctxs[0]
     spec_active, spec_ms = ctx.specialized()
     order_active, order_ms = ctx.tile_order_info()
     bvh = bool(ctx.scene_info() & pkg.abi.RT_INFO_BVH)
@@ -230,20 +265,20 @@ def main():
         band = tuple(int(v) for v in args.rows.split(":"))
         mode = "band"
     # strong scaling over several ranks: frame k's gather overlaps frame k+1's render
-    dr = pkg.dist.DistributedRenderer(ctx, packed, rank, world, dev, mode=mode, band=band,
+    dr = pkg.dist.DistributedRenderer(ctxs, packed, rank, world, dev, mode=mode, band=band,
                                       pipeline=args.scaling == "strong")
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, args.inflight)):  # every context warmed up
         dr.step()
     dr.flush()
     torch.cuda.synchronize()
-    ctx.read_stats(reset=True)
+    dr.read_stats(reset=True)
 
-    # Kernel time: torch events on the launch stream around each render launch
+    # Kernel time: torch events on the launch streams around each render launch
     # inside the timed region, read after it (no host sync per step).
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -257,12 +292,16 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kernel_ms = [e0.elapsed_time(e1) for e0, e1 in evs] if dr.has_work() else []
-    st = ctx.read_stats(reset=True)
+    launch_ms = [e0.elapsed_time(e1) for e0, e1 in evs] if dr.has_work() else []
+    span_ms = gpu_span_ms(evs) if dr.has_work() else 0.0
+    st = dr.read_stats(reset=True)
 
     rays_local = st.total_rays()
     flops_local = pkg.abi.algorithmic_flops(st, len(rargs.lights))
-    kavg = sum(kernel_ms) / len(kernel_ms) if kernel_ms else 0.0
+    # the roofline's kernel time: GPU span per frame (= the average launch
+    # duration when launches do not overlap, i.e. --inflight 1)
+    kavg = span_ms
+    lavg = sum(launch_ms) / len(launch_ms) if launch_ms else 0.0
     mx, sm = pkg.dist.reduce_max_sum([elapsed, rays_local], device=dev)
     elapsed, rays_total = mx[0], sm[1]
 
@@ -271,8 +310,8 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_total / elapsed / 1e6
         # roofline for the dominant (only) kernel: algorithmic FP64 flops per
-        # launch / average launch duration (HIP events on the launch stream)
-        flops_per_launch = flops_local / max(1, len(kernel_ms))
+        # launch / GPU time per launch (HIP events on the launch streams)
+        flops_per_launch = flops_local / max(1, len(launch_ms))
         achieved_tf = flops_per_launch / (kavg * 1e-3) / 1e12 if kavg > 0 else 0.0
         out_bytes = dr.buf.numel()
         line = {
@@ -295,6 +334,7 @@ def main():
                        "parallelism": ("rows %d:%d (band)" % band) if band else
                                       ("frame-per-gpu%d" % world) if args.scaling == "weak"
                                       else "rows%d-%s%s" % (world, args.shard, "-pipelined" if dr.pipeline else ""),
+                       "frames_in_flight": args.inflight,
                        "kernel": "specialised" if spec_active else "generic",
                        "accel": "bvh+cull" if args.accel == "bvh" else "none (brute force)",
                        "spec_compile_ms": round(spec_ms, 1),
@@ -309,6 +349,9 @@ def main():
                          "reference_work_frac": round(achieved_tf / PEAK_FP64_TFLOPS, 4),
                          "frac_nofma_ceiling": None if (bvh or no_ref_model) else round(achieved_tf / PEAK_FP64_NOFMA_TFLOPS, 4),
                          "kernel_ms": round(kavg, 4), "flops_per_launch": int(flops_per_launch),
+                         "kernel_ms_def": "GPU span per launch: first launch's start to the last end "
+                                          "(HIP events on the launch streams) / launches",
+                         "launch_ms_overlapped": round(lavg, 4),
                          "hbm_out_gbs": round(out_bytes / (kavg * 1e-3) / 1e9, 2) if kavg > 0 else None,
                          "traffic": None, "traffic_source": None},
             "cpu_baseline": None,
@@ -339,7 +382,7 @@ def main():
             line["roofline"]["traffic"] = int(tb)
             line["roofline"]["traffic_source"] = src
         if world == 1 and args.config == "c3" and args.companion == "auto" and not (args.width or args.height or band):
-            line["c3cone"] = side_config(pkg, "c3cone", dev, args.specialize == "on")
+            line["c3cone"] = side_config(pkg, "c3cone", dev, args.specialize == "on", args.inflight)
         if world == 1 and args.cpu_baseline == "auto":
             line["cpu_baseline"] = cpu_baseline(packed, args.cpu_threads)
         print(json.dumps(line), flush=True)

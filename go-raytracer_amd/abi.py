@@ -181,3 +181,20 @@ def algorithmic_flops(stats, num_lights):
         f += (int(stats.tests[k]) + int(stats.shadow_tests[k])) * FLOPS_PER_TEST[k]
     f += int(stats.shaded_hits) * (FLOPS_PER_SHADE + FLOPS_PER_LIGHT * num_lights)
     return f
+
+
+def sum_stats(stats):
+    """One rt_stats holding the field-wise sum of several (the counters of the
+    contexts that rendered frames in flight); kernel_ms is the largest."""
+    out = rt_stats()
+    for st in stats:
+        out.primary_rays += st.primary_rays
+        out.secondary_rays += st.secondary_rays
+        out.shadow_rays += st.shadow_rays
+        for k in range(RT_NUM_KINDS):
+            out.tests[k] += st.tests[k]
+            out.shadow_tests[k] += st.shadow_tests[k]
+        out.shaded_hits += st.shaded_hits
+        out.surface_errors += st.surface_errors
+        out.kernel_ms = max(out.kernel_ms, st.kernel_ms)
+    return out

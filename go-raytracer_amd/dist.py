@@ -130,11 +130,30 @@ def reduce_max_sum(values, device=None):
 class DistributedRenderer:
     """Per step: this rank's whole frame (mode "frame", weak scaling), or its
     share of one frame's rows ("interleaved" / "bands", strong scaling) followed
-    by the gather to rank 0."""
+    by the gather to rank 0.
 
-    def __init__(self, ctx, packed, rank, world, device, mode="interleaved", band=None, pipeline=False):
+    Frames in flight: `ctx` may be a list of F render contexts holding the same
+    scene (each with its own queue heads, frame stack and counters; rt_abi.h
+    contexts are independent). Step k renders on context k mod F, on that
+    context's stream, into buffer k mod F, so frame k+1's workgroups take the
+    CUs that frame k's last waves leave idle -- the tail of a launch (a
+    persistent grid draining its tile queue) overlaps the head of the next.
+    Every frame is still rendered whole; pixels and counters do not change.
+    F = 1 is the serial schedule on the caller's current stream."""
+
+    def __init__(self, ctx, packed, rank, world, device, mode="interleaved", band=None, pipeline=False,
+                 streams=None):
         import torch
-        self.ctx = ctx
+        self.ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx]
+        if not self.ctxs:
+            raise ValueError("no render context")
+        self.ctx = self.ctxs[0]
+        self.inflight = len(self.ctxs)
+        if streams is None:
+            streams = [None] if self.inflight == 1 else [torch.cuda.Stream(device) for _ in self.ctxs]
+        if len(streams) != self.inflight:
+            raise ValueError("one stream per context")
+        self.streams = list(streams)
         self.packed = packed
         self.rank = rank
         self.world = world
@@ -161,13 +180,16 @@ class DistributedRenderer:
             self.y0, self.y1, rows = band_rows(self.H, rank, world)
         self.buf = torch.zeros((rows, self.W, 4), dtype=torch.uint8, device=device)
         self.frame = None
-        # pipeline (strong scaling over >1 rank): two rank buffers alternate and
+        # pipeline (strong scaling over >1 rank): rank buffers alternate and
         # each gather runs asynchronously, so frame k's gather overlaps frame
         # k+1's render; a buffer is reused only after its gather has completed
         # (pipeline="always": also at one rank -- the GPU test of the RCCL path)
         self.pipeline = (pipeline == "always" or (bool(pipeline) and world > 1)) and mode in ("interleaved", "bands")
-        self.bufs = [self.buf, torch.zeros_like(self.buf)] if self.pipeline else [self.buf]
-        self.pending = [None] * len(self.bufs)
+        nbufs = max(self.inflight, 2 if self.pipeline else 1)
+        if nbufs % self.inflight:
+            raise ValueError("buffers must divide evenly over the contexts")
+        self.bufs = [self.buf] + [torch.zeros_like(self.buf) for _ in range(nbufs - 1)]
+        self.pending = [None] * nbufs
         self.k = 0
 
     def has_work(self):
@@ -175,48 +197,68 @@ class DistributedRenderer:
             return True
         return self.ntrows > 0 if self.mode == "interleaved" else self.y1 > self.y0
 
+    def read_stats(self, reset=True):
+        """Counters of every context, summed (abi.sum_stats)."""
+        from . import abi
+        return abi.sum_stats([c.read_stats(reset=reset) for c in self.ctxs])
+
     def step(self, gather=True, events=None, collective=None):
         """Render this rank's rows and gather the frame. `events` (start, end):
         torch.cuda.Events recorded on the launch stream around the render
         kernel, for kernel timing without a host sync per step."""
-        if events is not None:
-            events[0].record()
-        if self.mode in ("frame", "band"):
-            if self.mode == "frame":
-                self.ctx.render_rows_async(0, self.H, self.buf)
-            else:
-                self.ctx.render_rows_async(self.y0, self.y1, self.buf)
-            if events is not None:
-                events[1].record()
-            self.frame = self.buf  # rank-local rows; nothing to exchange
-            return self.frame
+        import torch
         slot = self.k % len(self.bufs)
+        i = self.k % self.inflight
         self.k += 1
+        ctx, stream, buf = self.ctxs[i], self.streams[i], self.bufs[slot]
         if self.pending[slot] is not None:  # this buffer's previous gather must be done
+            # completed (and the frame assembled) on the caller's stream, which
+            # the launch stream then follows before it overwrites the buffer
             self.frame = self.pending[slot].wait()
             self.pending[slot] = None
-        buf = self.bufs[slot]
-        if self.mode == "interleaved":
-            if self.ntrows > 0:
-                self.ctx.render_tile_rows_async(self.rank, self.world, self.ntrows,
-                                                buf[: self.ntrows * TILE])
-        elif self.y1 > self.y0:
-            self.ctx.render_rows_async(self.y0, self.y1, buf[: self.y1 - self.y0])
-        if events is not None:
-            events[1].record()
-        if gather:
-            if self.pipeline:
-                self.pending[slot] = gather_frame_async(buf, self.H, self.mode, slot)
-                return None  # the frame comes from flush() / a later step
-            self.frame = gather_frame(buf, self.H, self.mode, collective=collective)
+            if stream is not None:
+                stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            if events is not None:
+                events[0].record()
+            if self.mode in ("frame", "band"):
+                if self.mode == "frame":
+                    ctx.render_rows_async(0, self.H, buf, stream=stream)
+                else:
+                    ctx.render_rows_async(self.y0, self.y1, buf, stream=stream)
+                if events is not None:
+                    events[1].record()
+                self.frame = buf  # rank-local rows; nothing to exchange (complete after flush())
+                return self.frame
+            if self.mode == "interleaved":
+                if self.ntrows > 0:
+                    ctx.render_tile_rows_async(self.rank, self.world, self.ntrows,
+                                               buf[: self.ntrows * TILE], stream=stream)
+            elif self.y1 > self.y0:
+                ctx.render_rows_async(self.y0, self.y1, buf[: self.y1 - self.y0], stream=stream)
+            if events is not None:
+                events[1].record()
+            if gather:
+                if self.pipeline:
+                    # issued on the launch stream: the collective waits for this render only
+                    self.pending[slot] = gather_frame_async(buf, self.H, self.mode, slot)
+                    return None  # the frame comes from flush() / a later step
+                self.frame = gather_frame(buf, self.H, self.mode, collective=collective)
         return self.frame
 
     def flush(self):
         """Complete every in-flight gather (pipeline mode); returns the frame of
-        the last step on rank 0."""
+        the last step on rank 0. Frames in flight: the caller's stream is
+        ordered after every context's stream."""
+        import torch
         order = [(self.k + i) % len(self.bufs) for i in range(len(self.bufs))]  # oldest first
         for slot in order:
             if self.pending[slot] is not None:
                 self.frame = self.pending[slot].wait()
                 self.pending[slot] = None
+        if self.inflight > 1 and torch.cuda.is_available():
+            cur = torch.cuda.current_stream()
+            for s in self.streams:
+                if s is not None:
+                    cur.wait_stream(s)
         return self.frame

@@ -7,7 +7,7 @@ CFG=${1:-c3}
 O=gpurun_out/pmc_$CFG
 mkdir -p $O
 export TMPDIR=/tmp
-B="python3 bench.py --config $CFG --steps 2 --warmup 1 --cpu-baseline off --companion off ${PMC_BENCH_ARGS:-}"
+B="python3 bench.py --config $CFG --steps 2 --warmup 1 --inflight 1 --cpu-baseline off --companion off ${PMC_BENCH_ARGS:-}"
 timeout -k 10 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/cal_f -o cal_f --output-format csv -- ./build_variants/pmc_calib > /dev/null 2>&1 && \
 timeout -k 10 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/cal_w -o cal_w --output-format csv -- ./build_variants/pmc_calib > /dev/null 2>&1 && \
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d $O/p1 -o p1 --output-format csv -- $B > /dev/null 2>&1 && \

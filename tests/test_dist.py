@@ -93,12 +93,15 @@ class _OracleCtx:
 
     def __init__(self, packed, oracle_bind):
         self.packed, self.ob = packed, oracle_bind
+        self.calls = 0
 
     def render_rows_async(self, y0, y1, out, stream=None):
+        self.calls += 1
         img, _ = self.ob.render_rows(self.packed, y0, y1, threads=2)
         out[: y1 - y0] = torch.from_numpy(img)
 
     def render_tile_rows_async(self, trow0, stride, ntrows, out, stream=None):
+        self.calls += 1
         h = self.packed.height
         for j in range(ntrows):
             y0 = (trow0 + j * stride) * 8
@@ -157,7 +160,7 @@ def test_reduce_max_sum_without_process_group():
     assert rt.dist.reduce_max_sum([1.5, 2.0]) == ([1.5, 2.0], [1.5, 2.0])
 
 
-def _pipeline_worker(rank, world, port, w, h, q, mode):
+def _pipeline_worker(rank, world, port, w, h, q, mode, inflight=1):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -168,15 +171,17 @@ def _pipeline_worker(rank, world, port, w, h, q, mode):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     packed = pkg.scene.convert(pkg.configs.c2(width=w, height=h))
-    dr = pkg.dist.DistributedRenderer(_OracleCtx(packed, oracle_bind), packed, rank, world, "cpu", mode=mode,
-                                      pipeline=True)
-    assert dr.pipeline and len(dr.bufs) == 2
+    ctxs = [_OracleCtx(packed, oracle_bind) for _ in range(inflight)]
+    dr = pkg.dist.DistributedRenderer(ctxs if inflight > 1 else ctxs[0], packed, rank, world, "cpu", mode=mode,
+                                      pipeline=True, streams=[None] * inflight)
+    assert dr.pipeline and len(dr.bufs) == max(2, inflight) and dr.inflight == inflight
     frames = []
     for _ in range(3):  # step 3 reuses step 1's buffer: its gather completes first
         dr.step()
         if dr.frame is not None:
             frames.append(dr.frame.numpy().copy())
     last = dr.flush()
+    assert all(c.calls == len(range(i, 3, inflight)) for i, c in enumerate(ctxs))  # step k on context k mod F
     if rank == 0:
         frames.append(last.numpy().copy())
         q.put(frames)
@@ -184,11 +189,14 @@ def _pipeline_worker(rank, world, port, w, h, q, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "interleaved"), (3, "bands")])
-def test_pipelined_gather_frames_equal_full_frame(world, mode):
-    """bench.py --scaling strong over several ranks: two rank buffers alternate
+@pytest.mark.parametrize("world,mode,inflight", [(2, "interleaved", 1), (3, "bands", 1),
+                                                (2, "interleaved", 2), (3, "interleaved", 3)])
+def test_pipelined_gather_frames_equal_full_frame(world, mode, inflight):
+    """bench.py --scaling strong over several ranks: rank buffers alternate
     and each gather is asynchronous (frame k's gather overlaps frame k+1's
-    render); every gathered frame equals the full-frame render."""
+    render); with frames in flight (bench --inflight, the default 2) step k
+    renders on context k mod F into buffer k mod F. Every gathered frame
+    equals the full-frame render."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind
@@ -197,7 +205,8 @@ def test_pipelined_gather_frames_equal_full_frame(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, w, h, q, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, w, h, q, mode, inflight))
+             for r in range(world)]
     for p in procs:
         p.start()
     frames = q.get(timeout=180)
@@ -205,6 +214,8 @@ def test_pipelined_gather_frames_equal_full_frame(world, mode):
         p.join(timeout=120)
         assert p.exitcode == 0
     full, _ = oracle_bind.render_rows(rt.scene.convert(rt.configs.c2(width=w, height=h)))
-    assert len(frames) == 2  # step 3 completed step 1's gather; flush the last one
+    # with 2 buffers step 3 completed step 1's gather and flush the last one;
+    # with 3 buffers in flight only flush completes one
+    assert len(frames) == (2 if inflight < 3 else 1)
     for f in frames:
         assert np.array_equal(f, full)

@@ -85,3 +85,68 @@ def test_rccl_max_sum_reduction(nccl_group):
     import torch
     mx, sm = rt.dist.reduce_max_sum([1.5, 7.0], device=torch.device("cuda", 0))
     assert mx == [1.5, 7.0] and sm == [1.5, 7.0]
+
+
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_frames_in_flight_equal_serial_frames(inflight):
+    """bench.py --inflight F (default 2): F contexts with the same scene render
+    consecutive frames on F streams, so launches overlap on the device. Every
+    frame's pixels equal the serial render, and the summed counters equal the
+    serial counters times the frame count."""
+    import torch
+    packed = rt.scene.convert(rt.configs.c3(width=640, height=360))
+    dev = torch.device("cuda", 0)
+    ref = rt.RenderContext(0, specialize=True)
+    ctxs = [rt.RenderContext(0, specialize=True) for _ in range(inflight)]
+    try:
+        ref.set_scene(packed)
+        ref.read_stats(reset=True)
+        full = ref.render()
+        st1 = ref.read_stats(reset=True).as_dict()
+        for c in ctxs:
+            c.set_scene(packed)
+            c.read_stats(reset=True)
+        dr = rt.dist.DistributedRenderer(ctxs, packed, 0, 1, dev, mode="frame")
+        assert dr.inflight == inflight and len(dr.bufs) == inflight and len(set(dr.streams)) == inflight
+        steps = 2 * inflight + 1
+        for _ in range(steps):
+            dr.step()
+        dr.flush()
+        torch.cuda.synchronize()
+        for b in dr.bufs:
+            assert np.array_equal(b.cpu().numpy(), full)
+        st = dr.read_stats(reset=True).as_dict()
+        for k, v in st1.items():
+            want = [x * steps for x in v] if isinstance(v, list) else v * steps
+            assert st[k] == want, k
+    finally:
+        ref.close()
+        for c in ctxs:
+            c.close()
+
+
+def test_rccl_pipelined_gathers_with_frames_in_flight(nccl_group):
+    """The strong-scaling loop with two contexts in flight: each RCCL gather is
+    issued on its render's stream; every gathered frame equals the full render."""
+    import torch
+    packed = rt.scene.convert(rt.configs.c3(width=320, height=180))
+    ctxs = [rt.RenderContext(0) for _ in range(2)]
+    try:
+        for c in ctxs:
+            c.set_scene(packed)
+        full = ctxs[0].render()
+        dr = rt.dist.DistributedRenderer(ctxs, packed, 0, 1, torch.device("cuda", 0), mode="interleaved",
+                                         pipeline="always")
+        got = []
+        for _ in range(5):
+            dr.step()
+            if dr.frame is not None:
+                got.append(dr.frame.cpu().numpy())
+        got.append(dr.flush().cpu().numpy())
+        torch.cuda.synchronize()
+        assert len(got) == 4
+        for g in got:
+            assert np.array_equal(g, full)
+    finally:
+        for c in ctxs:
+            c.close()
