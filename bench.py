@@ -178,6 +178,7 @@ def make_contexts(pkg, dev, packed, n, specialize, accel=None):
         c = pkg.RenderContext(dev.index, specialize=specialize)
         if accel is not None:
             c.set_accel(accel)
+        c.set_frames_in_flight(n)  # the automatic schedule knows the launches overlap
         c.set_scene(packed)
         ctxs.append(c)
     return ctxs

@@ -474,6 +474,7 @@ struct rt_context {
   int device = 0;
   int last_waves = 0, launches = 0;  // diagnostics (RT_PHASE_TIMING wave lifetimes)
   int sched = RT_SCHED_AUTO;         // rt_set_schedule
+  int inflight = 1;                  // rt_set_frames_in_flight: launches overlap other contexts' launches
   LaunchPlan plan;                   // last launch's occupancy / LDS plan
   unsigned long long* wdiag = nullptr;  // diagnostic build: per-wave lifetimes (RT_PHASE_TIMING)
   int cus = 0;
@@ -720,15 +721,23 @@ void csg_mask_program(const int* code, int len, std::vector<int>& out) {
 // per lane (C2 over 4 / 8 ranks: 0.22 / 0.19 vs 0.18 / 0.14 ms). Otherwise the
 // idle siblings cost more than the balance gains (C3 whole frame 3.44 vs
 // 4.39 ms, C2 0.38 vs 0.45 ms).
+// With frames in flight (rt_set_frames_in_flight >= 2) the next frame's
+// workgroups fill the CUs a launch's tail leaves idle, so for a launch with
+// many pixels per lane the cheaper serial schedule wins even at depth >= 7 on
+// LDS scenes without CSG (C4 whole frame, two in flight: 4.25 ms serial vs
+// 5.09 ms quads); CSG keeps quads (c4csg 23.5 vs 12.8 ms), and so do scenes
+// read from HBM (not measured) and launches with few pixels per lane.
 // rt_set_schedule overrides the choice; so does RT_PIXEL_QUADS=0/1 in the
 // environment at process start (experiments).
-bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus) {
+bool scene_in_lds(const DevScene& s);
+bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus, int inflight) {
   static const int env = getenv("RT_PIXEL_QUADS") ? atoi(getenv("RT_PIXEL_QUADS")) : -1;
   if (env >= 0) return env != 0;
   if (sched == RT_SCHED_PIXEL) return false;
   if (sched == RT_SCHED_QUADS) return true;
   const double lanes = (double)std::max(1, cus) * 4 * 3 * 64;  // 3 waves per SIMD
-  return s.depth >= 7 || (double)pixels < (s.branching ? 16.0 : 4.0) * lanes;
+  const bool deep = s.depth >= 7 && !(inflight > 1 && scene_in_lds(s) && !s.has_csg);
+  return deep || (double)pixels < (s.branching ? 16.0 : 4.0) * lanes;
 }
 
 bool scene_in_lds(const DevScene& s) {
@@ -858,7 +867,7 @@ int spec_prepare(rt_context* c) {
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
-  sk.quads = use_quads(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus) ? 1 : 0;
+  sk.quads = use_quads(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus, c->inflight) ? 1 : 0;
   sk.share = c->share_on ? 1 : 0;
   c->spec_key = sk;
   c->spec_alt_fn = nullptr;
@@ -904,6 +913,13 @@ int rt_set_schedule(rt_context* c, int mode) {
     return fail(RT_E_INVALID, "rt_set_schedule: unknown mode");
   c->sched = mode;
   return RT_OK;
+}
+
+int rt_set_frames_in_flight(rt_context* c, int n) {
+  if (!c) return fail(RT_E_INVALID, "rt_set_frames_in_flight: NULL context");
+  if (n < 1) return fail(RT_E_INVALID, "rt_set_frames_in_flight: n < 1");
+  c->inflight = n;
+  return c->has_scene ? spec_prepare(c) : RT_OK;
 }
 
 int rt_set_specialize(rt_context* c, int enable) {
@@ -1585,7 +1601,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
-  const bool quads = !est && use_quads(c->sched, s, launch_pixels, c->cus);
+  const bool quads = !est && use_quads(c->sched, s, launch_pixels, c->cus, c->inflight);
   const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
   hipFunction_t spec = nullptr;  // built for this scene's flavour (spec_key), this schedule
   {

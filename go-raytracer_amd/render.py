@@ -75,6 +75,8 @@ def load_library(path=None):
     l.rt_set_work_sharing.restype = i
     l.rt_set_tile_order.argtypes = [vp, i]
     l.rt_set_tile_order.restype = i
+    l.rt_set_frames_in_flight.argtypes = [vp, i]
+    l.rt_set_frames_in_flight.restype = i
     l.rt_tile_order_info.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_double)]
     l.rt_tile_order_info.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
@@ -155,6 +157,13 @@ class RenderContext:
         estimate -- one centre sample per 8x8 tile -- runs at scene setup);
         identical pixels and counters either way. Applies at once."""
         _check(self.lib.rt_set_tile_order(self.handle, int(bool(enable))), "rt_set_tile_order")
+
+    def set_frames_in_flight(self, n):
+        """This context is one of n whose launches overlap (frames in flight,
+        dist.DistributedRenderer with a list of contexts): the automatic
+        schedule may then prefer serial samples at depth >= 7. Identical
+        pixels and counters. Applies at once."""
+        _check(self.lib.rt_set_frames_in_flight(self.handle, int(n)), "rt_set_frames_in_flight")
 
     def set_work_sharing(self, enable=True):
         """Work sharing at the tail of a launch (specialised kernel only;

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 #define RT_EXP_AMD64_FMA 0
 #define RT_EXP_AMD64 1
 #define RT_EXP_PORTABLE 2
@@ -345,6 +345,16 @@ int rt_set_accel(rt_context *ctx, int flags);
 #define RT_SCHED_PIXEL 1
 #define RT_SCHED_QUADS 2
 int rt_set_schedule(rt_context *ctx, int mode);
+
+/* Frames in flight (MI355X-specific; pixels and counters are identical): a
+ * host rendering a stream of frames keeps n >= 2 contexts with the same scene
+ * and alternates its launches over them, one stream each, so one frame's
+ * last waves share the chip with the next frame's first.
+ * Telling each context n lets RT_SCHED_AUTO pick the serial schedule for
+ * whole frames at depth >= 7 (scenes in LDS without CSG), whose tail the
+ * overlap then hides. Default 1. Takes effect at once. No reference
+ * counterpart (Render is one synchronous frame, raytracer.go:589). */
+int rt_set_frames_in_flight(rt_context *ctx, int n);
 
 /* Tile order (MI355X-specific; pixels and counters are identical either
  * way). With enable != 0 (default) rt_set_scene also traces sample 0 of four

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/final3
+O=${O:-gpurun_out/final3}
 mkdir -p $O/sweep $O/strong
 for c in ${SWEEP_CFGS:-c1 c2 canned c3 c3cone c4 c4csg c5}; do
   steps=10; [ $c = c5 ] && steps=3; [ $c = c4csg ] && steps=5
@@ -13,5 +13,9 @@ done
 for c in ${STRONG_CFGS:-c3 c3cone c4 c2}; do
   STRONG_WORLDS=1,2,4,8 timeout -k 10 300 python3 scripts/strong_emul.py $c 10 > $O/strong/$c.json 2> $O/strong/$c.err || { tail -5 $O/strong/$c.err; exit 1; }
   cat $O/strong/$c.json
+done
+for c in ${INFLIGHT_CFGS:-c3 c3cone c4 c2}; do
+  INFLIGHT_F=${INFLIGHT_F:-1,2,3} timeout -k 10 400 python3 scripts/inflight_emul.py $c 20 > $O/strong/inflight_$c.json 2> $O/strong/inflight_$c.err || { tail -5 $O/strong/inflight_$c.err; exit 1; }
+  cat $O/strong/inflight_$c.json
 done
 timeout -k 10 700 python3 -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; tail -1 $O/pytest_gpu.log

@@ -6,7 +6,8 @@ leaves idle. F = 1 is the serial baseline (one context, one stream).
 w<N>_f<F>_eff_max = t(1 rank, F) / (N * slowest rank's share time at F): the
 efficiency the driver's 1/2/4/8-GPU bench lines give (every line runs F).
 usage: python scripts/inflight_emul.py [config] [steps]
-       (INFLIGHT_WORLDS=1,8  INFLIGHT_F=1,2,3  INFLIGHT_RANKS=all|0)"""
+       (INFLIGHT_WORLDS=1,8  INFLIGHT_F=1,2,3  INFLIGHT_RANKS=all|0  INFLIGHT_HINT=1|0:
+        rt_set_frames_in_flight(F) on the contexts, as bench.py does)"""
 import json
 import os
 import sys
@@ -40,6 +41,9 @@ def main():
         drs = [pkg.dist.DistributedRenderer(ctxs[i], packed, rank, world, dev, mode="interleaved")
                for i in range(F)]
         nt = drs[0].ntrows
+        if os.environ.get("INFLIGHT_HINT", "1") == "1":  # rt_set_frames_in_flight, as bench.py does
+            for c in ctxs[:F]:
+                c.set_frames_in_flight(F)
 
         def launch(k):
             i = k % F

@@ -141,3 +141,25 @@ def test_launches_on_alternating_streams(ctxs):
     for key, v in ost.as_dict().items():
         want = [6 * x for x in v] if isinstance(v, (list, tuple)) else 6 * v
         assert st.as_dict()[key] == want, key
+
+
+@pytest.mark.parametrize("specialize", [False, True])
+def test_frames_in_flight_hint_keeps_bytes_and_counters(specialize):
+    """rt_set_frames_in_flight(ctx, 2) lets the automatic schedule deal a whole
+    4K C4 frame (depth 8, LDS scene, no CSG) serially instead of in pixel
+    quads; the frame and every counter equal the default schedule's (which
+    the full-size oracle tests pin)."""
+    packed = rt.scene.convert(rt.configs.c4())
+    a = rt.RenderContext(0, specialize=specialize)
+    b = rt.RenderContext(0, specialize=specialize)
+    try:
+        b.set_frames_in_flight(2)
+        ref, st_ref = render(a, packed)
+        img, st = render(b, packed)
+        assert_same(img, ref, "C4 serial (frames in flight) vs quads")
+        assert st.as_dict() == st_ref.as_dict()
+        with pytest.raises(rt.render.RenderError):
+            b.set_frames_in_flight(0)
+    finally:
+        a.close()
+        b.close()
