@@ -70,6 +70,10 @@ def parse():
                    help="frames in flight per rank: F render contexts with the same scene on F streams "
                         "render consecutive frames round-robin, so one frame's tail overlaps the next "
                         "frame's head (every frame still rendered whole; 1 = serial launches)")
+    p.add_argument("--schedule", choices=["auto", "pixel", "quads"], default="auto",
+                   help="rt_set_schedule: how pixels are dealt to lanes (identical pixels and counters); "
+                        "auto picks from depth, pixels per lane and frames in flight. The PMC passes run "
+                        "--inflight 1 with the schedule the in-flight bench picks")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -172,12 +176,14 @@ def gpu_span_ms(evs):
     return span / len(evs)
 
 
-def make_contexts(pkg, dev, packed, n, specialize, accel=None):
+def make_contexts(pkg, dev, packed, n, specialize, accel=None, schedule="auto"):
     ctxs = []
     for _ in range(n):
         c = pkg.RenderContext(dev.index, specialize=specialize)
         if accel is not None:
             c.set_accel(accel)
+        c.set_schedule({"auto": pkg.abi.RT_SCHED_AUTO, "pixel": pkg.abi.RT_SCHED_PIXEL,
+                        "quads": pkg.abi.RT_SCHED_QUADS}[schedule])
         c.set_frames_in_flight(n)  # the automatic schedule knows the launches overlap
         c.set_scene(packed)
         ctxs.append(c)
@@ -251,7 +257,7 @@ def main():
     if args.inflight < 1:
         raise SystemExit("--inflight must be >= 1")
     ctxs = make_contexts(pkg, dev, packed, args.inflight, args.specialize == "on",
-                         accel=0 if args.accel == "none" else None)
+                         accel=0 if args.accel == "none" else None, schedule=args.schedule)
     ctx = ctxs[0]
     spec_active, spec_ms = ctx.specialized()
     order_active, order_ms = ctx.tile_order_info()
@@ -336,6 +342,7 @@ def main():
                                       ("frame-per-gpu%d" % world) if args.scaling == "weak"
                                       else "rows%d-%s%s" % (world, args.shard, "-pipelined" if dr.pipeline else ""),
                        "frames_in_flight": args.inflight,
+                       "schedule": args.schedule,
                        "kernel": "specialised" if spec_active else "generic",
                        "accel": "bvh+cull" if args.accel == "bvh" else "none (brute force)",
                        "spec_compile_ms": round(spec_ms, 1),

@@ -724,9 +724,10 @@ void csg_mask_program(const int* code, int len, std::vector<int>& out) {
 // With frames in flight (rt_set_frames_in_flight >= 2) the next frame's
 // workgroups fill the CUs a launch's tail leaves idle, so for a launch with
 // many pixels per lane the cheaper serial schedule wins even at depth >= 7 on
-// LDS scenes without CSG (C4 whole frame, two in flight: 4.25 ms serial vs
-// 5.09 ms quads); CSG keeps quads (c4csg 23.5 vs 12.8 ms), and so do scenes
-// read from HBM (not measured) and launches with few pixels per lane.
+// LDS scenes without CSG when a launch gives each lane >= 32 pixels (C4 whole
+// frame, 42 px/lane, two in flight: 4.23 ms serial vs 5.09 ms quads); CSG
+// keeps quads (c4csg 23.5 vs 12.8 ms), and so do scenes read from HBM (not
+// measured) and launches with fewer pixels per lane.
 // rt_set_schedule overrides the choice; so does RT_PIXEL_QUADS=0/1 in the
 // environment at process start (experiments).
 bool scene_in_lds(const DevScene& s);
@@ -736,8 +737,9 @@ bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus, int infli
   if (sched == RT_SCHED_PIXEL) return false;
   if (sched == RT_SCHED_QUADS) return true;
   const double lanes = (double)std::max(1, cus) * 4 * 3 * 64;  // 3 waves per SIMD
-  const bool deep = s.depth >= 7 && !(inflight > 1 && scene_in_lds(s) && !s.has_csg);
-  return deep || (double)pixels < (s.branching ? 16.0 : 4.0) * lanes;
+  if (s.depth >= 7 && inflight > 1 && scene_in_lds(s) && !s.has_csg)
+    return (double)pixels < 32.0 * lanes;  // C4 over 2 ranks (21 px/lane): 2.87 ms serial vs 2.44 quads
+  return s.depth >= 7 || (double)pixels < (s.branching ? 16.0 : 4.0) * lanes;
 }
 
 bool scene_in_lds(const DevScene& s) {

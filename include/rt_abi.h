@@ -351,8 +351,8 @@ int rt_set_schedule(rt_context *ctx, int mode);
  * and alternates its launches over them, one stream each, so one frame's
  * last waves share the chip with the next frame's first.
  * Telling each context n lets RT_SCHED_AUTO pick the serial schedule for
- * whole frames at depth >= 7 (scenes in LDS without CSG), whose tail the
- * overlap then hides. Default 1. Takes effect at once. No reference
+ * launches of >= 32 pixels per lane at depth >= 7 (whole frames; scenes in
+ * LDS without CSG), whose tail the overlap then hides. Default 1. Takes effect at once. No reference
  * counterpart (Render is one synchronous frame, raytracer.go:589). */
 int rt_set_frames_in_flight(rt_context *ctx, int n);
 
