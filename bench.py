@@ -190,16 +190,19 @@ def make_contexts(pkg, dev, packed, n, specialize, accel=None, schedule="auto"):
     return ctxs
 
 
-def side_config(pkg, name, dev, specialize, inflight, steps=10, warmup=2):
+def side_config(pkg, name, dev, specialize, inflight, streams=None, steps=10, warmup=2):
     """One GPU, whole frames of another config (the C3 line's companion: C3 as
     BASELINE.json states it, with the cone the reference lacks), with the same
-    frames in flight as the main line: value, ms/frame and the reference-work
-    roofline fraction."""
+    frames in flight as the main line, on the main line's streams (HIP maps
+    streams onto GPU_MAX_HW_QUEUES = 4 hardware queues round-robin: two more
+    streams can land on one queue, which serialises their launches): value,
+    ms/frame and the reference-work roofline fraction."""
     import torch
     rargs = pkg.configs.CONFIGS[name]()
     packed = pkg.scene.convert(rargs)
     ctxs = make_contexts(pkg, dev, packed, inflight, specialize)
-    dr = pkg.dist.DistributedRenderer(ctxs, packed, 0, 1, dev, mode="frame")
+    dr = pkg.dist.DistributedRenderer(ctxs, packed, 0, 1, dev, mode="frame",
+                                      streams=streams if inflight > 1 else None)
     for _ in range(max(warmup, inflight)):
         dr.step()
     dr.flush()
@@ -390,7 +393,7 @@ def main():
             line["roofline"]["traffic"] = int(tb)
             line["roofline"]["traffic_source"] = src
         if world == 1 and args.config == "c3" and args.companion == "auto" and not (args.width or args.height or band):
-            line["c3cone"] = side_config(pkg, "c3cone", dev, args.specialize == "on", args.inflight)
+            line["c3cone"] = side_config(pkg, "c3cone", dev, args.specialize == "on", args.inflight, streams=dr.streams)
         if world == 1 and args.cpu_baseline == "auto":
             line["cpu_baseline"] = cpu_baseline(packed, args.cpu_threads)
         print(json.dumps(line), flush=True)
