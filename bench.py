@@ -70,7 +70,7 @@ def parse():
                    help="frames in flight per rank: F render contexts with the same scene on F streams "
                         "render consecutive frames round-robin, so one frame's tail overlaps the next "
                         "frame's head (every frame still rendered whole; 1 = serial launches)")
-    p.add_argument("--schedule", choices=["auto", "pixel", "quads"], default="auto",
+    p.add_argument("--schedule", choices=["auto", "pixel", "quads", "pairs"], default="auto",
                    help="rt_set_schedule: how pixels are dealt to lanes (identical pixels and counters); "
                         "auto picks from depth, pixels per lane and frames in flight. The PMC passes run "
                         "--inflight 1 with the schedule the in-flight bench picks")
@@ -183,7 +183,7 @@ def make_contexts(pkg, dev, packed, n, specialize, accel=None, schedule="auto"):
         if accel is not None:
             c.set_accel(accel)
         c.set_schedule({"auto": pkg.abi.RT_SCHED_AUTO, "pixel": pkg.abi.RT_SCHED_PIXEL,
-                        "quads": pkg.abi.RT_SCHED_QUADS}[schedule])
+                        "quads": pkg.abi.RT_SCHED_QUADS, "pairs": pkg.abi.RT_SCHED_PAIRS}[schedule])
         c.set_frames_in_flight(n)  # the automatic schedule knows the launches overlap
         c.set_scene(packed)
         ctxs.append(c)

@@ -455,7 +455,7 @@ struct SpecKey {
   int kmask = 0, feat = 0, nlights = 0;  // nlights > 0: light loop unrolled for that count
   int pow_bits = 7;                      // unrolled specular powering steps
   int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
-  int quads = 0;                         // pixel quads (use_quads)
+  int quads = 0;                         // pixel schedule: SCH_SERIAL / SCH_QUADS / SCH_PAIRS (pick_schedule)
   int share = 0;                         // work sharing at the tail (rt_set_work_sharing): -DRT_SHARE=1
   std::string str() const {
     return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
@@ -515,7 +515,7 @@ struct rt_context {
   bool specialize = false;
   int accel = RT_ACCEL_BVH | RT_ACCEL_CULL;  // rt_set_accel
   hipFunction_t spec_fn = nullptr;  // specialised kernel of the current scene, if any
-  hipFunction_t spec_alt_fn = nullptr;  // ... for the other pixel schedule (spec_for)
+  hipFunction_t spec_alt_fn[3] = {nullptr, nullptr, nullptr};  // ... for the other pixel schedules (spec_for)
   SpecKey spec_key;                     // what spec_fn was compiled for
   double spec_ms = 0;               // hipRTC compile time of spec_fn (0 = cache hit)
 };
@@ -742,6 +742,32 @@ bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus, int infli
   return s.depth >= 7 || (double)pixels < (s.branching ? 16.0 : 4.0) * lanes;
 }
 
+// Pixel schedules of a launch (SpecKey.quads): serial samples, pixel quads,
+// or pixel pairs -- a pixel's samples 0-1 in one lane and 2-3 in its
+// neighbour, summed in sample order by the first (specialised kernels only,
+// -DRT_PAIRS=1; the generic kernels run quads instead). Pairs are chosen by
+// rt_set_schedule(RT_SCHED_PAIRS) or RT_PIXEL_PAIRS=1 in the environment
+// (experiments), and by RT_SCHED_AUTO with frames in flight for branching LDS
+// scenes without CSG (two in flight, ms per slowest rank's share,
+// profiles/r03/pairs/): depth < 7 from 8 to 16 pixels per lane (C3 over 4
+// ranks: 0.849 pairs vs 0.937 quads; over 8, 5 px/lane, 0.447 vs 0.451;
+// over 2, 21 px/lane, serial 1.575 vs 1.706), depth >= 7 from 16 (C4 whole
+// frame 4.15 vs 4.25 serial, over 2 ranks 2.08 vs 2.46 quads; over 4,
+// 10 px/lane, quads 1.16 vs 1.39).
+enum { SCH_SERIAL = 0, SCH_QUADS = 1, SCH_PAIRS = 2 };
+int pick_schedule(int sched, const DevScene& s, uint64_t pixels, int cus, int inflight, bool spec) {
+  static const int env = getenv("RT_PIXEL_PAIRS") ? atoi(getenv("RT_PIXEL_PAIRS")) : -1;
+  if (env > 0 || sched == RT_SCHED_PAIRS) return SCH_PAIRS;
+  static const int qenv = getenv("RT_PIXEL_QUADS") ? atoi(getenv("RT_PIXEL_QUADS")) : -1;
+  if (sched == RT_SCHED_AUTO && qenv < 0 && env < 0 && spec && inflight > 1 && scene_in_lds(s) && !s.has_csg &&
+      s.branching) {
+    const double ppl = (double)pixels / ((double)std::max(1, cus) * 4 * 3 * 64);  // pixels per lane
+    if (s.depth >= 7) return ppl >= 16.0 ? SCH_PAIRS : SCH_QUADS;
+    if (ppl >= 8.0 && ppl < 16.0) return SCH_PAIRS;
+  }
+  return use_quads(sched, s, pixels, cus, inflight) ? SCH_QUADS : SCH_SERIAL;
+}
+
 bool scene_in_lds(const DevScene& s) {
   static const bool force_global = getenv("RT_SCENE_GLOBAL") && atoi(getenv("RT_SCENE_GLOBAL")) != 0;
   return !force_global && s.blob_bytes <= (int)LDS_MAX_BYTES;
@@ -783,6 +809,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   defs.push_back("-DRT_SPEC_POWBITS=" + std::to_string(sk.pow_bits));
   if (sk.nocull) defs.push_back("-DRT_CULL=0");
   if (sk.share) defs.push_back("-DRT_SHARE=1");
+  if (sk.quads == SCH_PAIRS) defs.push_back("-DRT_PAIRS=1");
   std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
   for (const auto& d : defs) opts.push_back(d.c_str());
   // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only)
@@ -802,7 +829,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   for (const auto& x : extra) opts.push_back(x.c_str());
   const std::string name = std::string("rt_render_kernel<") + (sk.lds ? "true" : "false") + ", " +
                            (sk.bvh ? "true" : "false") + ", " + (sk.csg ? "true" : "false") + ", " +
-                           (sk.quads ? "true" : "false") + ">";
+                           (sk.quads == SCH_QUADS ? "true" : "false") + ">";
   const char* name_expr = name.c_str();
   hiprtcProgram prog;
   hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
@@ -869,30 +896,32 @@ int spec_prepare(rt_context* c) {
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
-  sk.quads = use_quads(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus, c->inflight) ? 1 : 0;
+  sk.quads = pick_schedule(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus, c->inflight, true);
+  if (sk.share && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the board assumes one owner lane per pixel
   sk.share = c->share_on ? 1 : 0;
   c->spec_key = sk;
-  c->spec_alt_fn = nullptr;
+  for (auto& f : c->spec_alt_fn) f = nullptr;
   std::lock_guard<std::mutex> lock(g_spec_mu);
   return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
 }
 
 // The specialised kernel for `quads` (the scene's other schedule is compiled
 // on first use: a launch covering a small share of the frame).
-int spec_for(rt_context* c, bool quads, hipFunction_t* fn) {
-  if (!c->spec_fn || (c->spec_key.quads != 0) == quads) {
+int spec_for(rt_context* c, int sch, hipFunction_t* fn) {
+  if (c->spec_fn && c->spec_key.share && sch == SCH_PAIRS) sch = SCH_QUADS;
+  if (!c->spec_fn || c->spec_key.quads == sch) {
     *fn = c->spec_fn;
     return RT_OK;
   }
-  if (!c->spec_alt_fn) {
+  if (!c->spec_alt_fn[sch]) {
     SpecKey sk = c->spec_key;
-    sk.quads = quads ? 1 : 0;
+    sk.quads = sch;
     double ms = 0;
     std::lock_guard<std::mutex> lock(g_spec_mu);
-    int rc = spec_build(c->device, sk, &c->spec_alt_fn, &ms);
+    int rc = spec_build(c->device, sk, &c->spec_alt_fn[sch], &ms);
     if (rc != RT_OK) return rc;
   }
-  *fn = c->spec_alt_fn;
+  *fn = c->spec_alt_fn[sch];
   return RT_OK;
 }
 
@@ -911,7 +940,7 @@ int rt_set_accel(rt_context* c, int flags) {
 
 int rt_set_schedule(rt_context* c, int mode) {
   if (!c) return fail(RT_E_INVALID, "rt_set_schedule: NULL context");
-  if (mode != RT_SCHED_AUTO && mode != RT_SCHED_PIXEL && mode != RT_SCHED_QUADS)
+  if (mode != RT_SCHED_AUTO && mode != RT_SCHED_PIXEL && mode != RT_SCHED_QUADS && mode != RT_SCHED_PAIRS)
     return fail(RT_E_INVALID, "rt_set_schedule: unknown mode");
   c->sched = mode;
   return RT_OK;
@@ -1603,13 +1632,16 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
-  const bool quads = !est && use_quads(c->sched, s, launch_pixels, c->cus, c->inflight);
-  const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
+  const int sch =
+      est ? (int)SCH_SERIAL : pick_schedule(c->sched, s, launch_pixels, c->cus, c->inflight, c->spec_fn != nullptr);
   hipFunction_t spec = nullptr;  // built for this scene's flavour (spec_key), this schedule
   {
-    int rc = spec_for(c, quads, &spec);
+    int rc = spec_for(c, sch, &spec);
     if (rc != RT_OK) return rc;
   }
+  // the generic kernels have no pairs flavour: quads instead (same pixels)
+  const bool quads = sch == SCH_QUADS || (sch == SCH_PAIRS && !spec);
+  const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
   // the board is in LDS only for a kernel compiled with work sharing
   const bool share = spec && c->spec_key.share;
   const int stream_off = board_off + (share ? BOARD_BYTES : 0);

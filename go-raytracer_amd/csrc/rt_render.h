@@ -37,6 +37,13 @@
 #ifndef RT_PIX_BATCH
 #define RT_PIX_BATCH 1
 #endif
+// Pixel pairs (specialised kernels, the host's RT_SCHED_PAIRS): with the
+// serial-sample flavour (QUADS = false), a pixel's samples 0-1 run in an even
+// lane and 2-3 in the odd lane after it; the even lane adds the four colours
+// in sample order.
+#ifndef RT_PAIRS
+#define RT_PAIRS 0
+#endif
 #ifndef RT_FRAME_PREFETCH
 #define RT_FRAME_PREFETCH 1  // load the parent frame during the TRACE pass
 #endif
@@ -1345,10 +1352,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef RT_COST_MAP
   constexpr bool QD = false;  // the cost-map diagnostic charges all of a pixel's work to one lane
+  constexpr bool PR = false;
 #else
   constexpr bool QD = QUADS;
+  constexpr bool PR = !QUADS && RT_PAIRS && !RT_SHARE;  // pixel pairs (the board assumes one owner lane)
 #endif
-  constexpr unsigned int QCHUNK = QD ? 16u : (unsigned int)RT_QCHUNK_PIXEL;
+  // pixels per dequeue: 16 quads, 32 pairs (an 8x4 half tile) or 64 pixels
+  constexpr unsigned int QCHUNK = QD ? 16u : PR ? 32u : (unsigned int)RT_QCHUNK_PIXEL;
   const char* base;
   // Stage the scene (LDS flavour) once per workgroup (the only block-wide
   // barrier).
@@ -1518,6 +1528,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   double hit_t = 0.0;
   Pcg rng{0, 0};
   d3 sum = mk(0, 0, 0);
+  d3 sum2 = mk(0, 0, 0);  // pixel pairs: the odd lane's sample-3 colour (sample 2's is in sum)
   Ray ray;
   ray.o = mk(0, 0, 0);
   ray.d = mk(0, 0, 1);
@@ -1582,6 +1593,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         state = S_IDLE;
         return;
       }
+      if (PR && sample == ((lane & 1) ? 4 : 2)) {  // this lane's two samples are done: the pair adds them
+        state = S_DONE;
+        return;
+      }
       if (sample == 4) {
         d3 c = scale(sum, 1.0 / 4.0);  // raytracer.go:656 -> vec.go:104-107
         uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
@@ -1640,8 +1655,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             state = S_DONE;
           } else {
             // raytracer.go:651 (a claimed sample's helper starts from sum = -0:
-            // -0 + c == c for every c, so sum is exactly its colour)
-            sum = add(sum, res);
+            // -0 + c == c for every c, so sum is exactly its colour); a pair's
+            // odd lane keeps samples 2 and 3 apart for the even lane's sum
+            if (PR && (lane & 1))
+              (sample == 2 ? sum : sum2) = res;
+            else
+              sum = add(sum, res);
             sample++;
             state = S_ADV;
           }
@@ -1746,7 +1765,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         // a lane about to finish a pixel while it still holds one: every
         // held pixel goes out in one store first (with sharing a lane may also
         // finish by taking helpers' colours, so any advancing holder flushes)
-        if (RT_PIX_BATCH && __any(state == S_ADV && held_px != ~0u && (RT_SHARE || sample == 4))) flush_pixels();
+        if (RT_PIX_BATCH && __any(state == S_ADV && held_px != ~0u && (RT_SHARE || (!PR && sample == 4)))) flush_pixels();
         if (state == S_ADV) {
           const uint32_t w = RT_SHARE ? Bd->lw[threadIdx.x] : 4u;
           if (RT_SHARE && __builtin_expect(lw_task(w) >= 0, 0)) {
@@ -1790,13 +1809,44 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if ((qd >> (lane & ~3)) & 1) state = S_IDLE;
       }
     }
+    // ---- pairs whose 4 samples are all done: the even lane adds
+    // (((0 + s0) + s1) + s2) + s3 -- its own running sum, then its
+    // neighbour's two colours (raytracer.go:651) -- and quantises
+    // (raytracer.go:656, vec.go:104-107); the pair becomes idle ----
+    if constexpr (PR) {
+      const uint64_t dn = __ballot(state == S_DONE);
+      const uint64_t pd = dn & (dn >> 1) & 0x5555555555555555ull;
+      if (pd) {
+        const int lb = (lane + 1) & 63;
+        const d3 c2 = mk(__shfl(sum.x, lb), __shfl(sum.y, lb), __shfl(sum.z, lb));
+        const d3 c3 = mk(__shfl(sum2.x, lb), __shfl(sum2.y, lb), __shfl(sum2.z, lb));
+        const d3 sm = add(add(sum, c2), c3);
+        if (RT_PIX_BATCH && __any(((pd >> lane) & 1) && held_px != ~0u)) flush_pixels();
+        if ((pd >> lane) & 1) {
+          const d3 c = scale(sm, 1.0 / 4.0);
+          const uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
+          const uint32_t g8 = go_f64_to_u32(c.y * 65535.0) >> 8;
+          const uint32_t b8 = go_f64_to_u32(c.z * 65535.0) >> 8;
+          const uint32_t v = (r8 & 0xffu) | ((g8 & 0xffu) << 8) | ((b8 & 0xffu) << 16) | 0xff000000u;
+          if (RT_PIX_BATCH) {
+            held_px = pout;
+            held_val = v;
+          } else {
+            P.out[pout] = v;
+          }
+        }
+        if ((pd >> (lane & ~1)) & 1) state = S_IDLE;
+      }
+    }
     // ---- refill idle lanes from the wave pool (one 8x8 tile per chunk) ----
     for (;;) {
       // with quads a pixel goes to a quad whose 4 lanes are all idle, sample k
       // to lane 4p+k; mask = the idle lanes / the idle quads' first lanes
       const uint64_t il = __ballot(state == S_IDLE);
-      const uint64_t mask = QD ? il & (il >> 1) & (il >> 2) & (il >> 3) & 0x1111111111111111ull : il;
-      const bool need = ((mask >> (QD ? (lane & ~3) : lane)) & 1) != 0;
+      const uint64_t mask = QD   ? il & (il >> 1) & (il >> 2) & (il >> 3) & 0x1111111111111111ull
+                            : PR ? il & (il >> 1) & 0x5555555555555555ull
+                                 : il;
+      const bool need = ((mask >> (QD ? (lane & ~3) : PR ? (lane & ~1) : lane)) & 1) != 0;
       if (mask == 0 || exhausted) break;
       if (pool_next >= pool_end) {
         const unsigned int nchunks = (P.total_slots + QCHUNK - 1) / QCHUNK;
@@ -1828,11 +1878,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         pool_end = min(pool_next + (unsigned int)QCHUNK, P.total_slots);
       }
       // idle lanes (quads) before mine
-      const unsigned int rank = QD ? (unsigned int)__popcll(mask & ((1ull << (lane & ~3)) - 1ull))
-                                   : __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
+      const unsigned int rank = QD   ? (unsigned int)__popcll(mask & ((1ull << (lane & ~3)) - 1ull))
+                                : PR ? (unsigned int)__popcll(mask & ((1ull << (lane & ~1)) - 1ull))
+                                     : __builtin_amdgcn_mbcnt_hi((unsigned int)(mask >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((unsigned int)mask, 0u));
       unsigned int take = min((unsigned int)__popcll(mask), pool_end - pool_next);
-      if (!QD && P.est_out) {  // cost estimate: unit u = pixel (u mod est_pts) of frame tile u / est_pts
+      if (!QD && !PR && P.est_out) {  // cost estimate: unit u = pixel (u mod est_pts) of frame tile u / est_pts
         if (need && rank < take) {
           const unsigned int u = pool_next + rank, t = u / (unsigned)P.est_pts, k = u % (unsigned)P.est_pts;
           px = min((int)(t % (unsigned)P.tiles_x) * TILE + est_x(P.est_pts, k), P.width - 1);
@@ -1876,8 +1927,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const int ry = r0t + ty >= 20 ? r0t + ty - 20 : r0t + ty;  // y % 20 (ty < 8)
           const int ymin = y - ry;
           Pcg s0{0xDEADULL ^ (uint64_t)x, 0xBEEFULL ^ (uint64_t)ymin};
-          sample = QD ? (lane & 3) : 0;
-          const uint64_t* j = QD ? P.jump + (ry * 4 + sample) * 4 : jrows + ry * 4;
+          sample = QD ? (lane & 3) : PR ? (lane & 1) * 2 : 0;
+          const uint64_t* j = (QD || PR) ? P.jump + (ry * 4 + sample) * 4 : jrows + ry * 4;
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sum = mk(0, 0, 0);
           sp = 0;
@@ -2231,7 +2282,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     // (a lane that finished a sample and starts the next one at the loop top,
     // S_ADV, counts as tracing: leaving it out ran SHADE with fewer lanes,
     // lane utilisation 0.83 -> 0.74 and C3 +5 %)
-    const uint64_t ntr = popc_ballot(state == S_TRACE || (!QD && state == S_ADV && (RT_SHARE || sample < 4)));
+    const uint64_t ntr = popc_ballot(state == S_TRACE ||
+                                     (!QD && state == S_ADV && (RT_SHARE || sample < (PR && !(lane & 1) ? 2 : 4))));
     if (nsh == 0 || (ntr != 0 && nsh * RT_SHADE_DEN < (nsh + ntr) * RT_SHADE_NUM)) continue;
 
     const bool hit = state == S_SHADE;

@@ -344,15 +344,22 @@ int rt_set_accel(rt_context *ctx, int flags);
 #define RT_SCHED_AUTO 0
 #define RT_SCHED_PIXEL 1
 #define RT_SCHED_QUADS 2
+/* RT_SCHED_PAIRS: a pixel's samples 0-1 in one lane and 2-3 in the next, the
+ * first lane adding all four in sample order -- half the quads' per-pixel
+ * parallelism at half their idle-lane cost (specialised kernels,
+ * rt_set_specialize; the generic kernels run quads for it). */
+#define RT_SCHED_PAIRS 3
 int rt_set_schedule(rt_context *ctx, int mode);
 
 /* Frames in flight (MI355X-specific; pixels and counters are identical): a
  * host rendering a stream of frames keeps n >= 2 contexts with the same scene
  * and alternates its launches over them, one stream each, so one frame's
  * last waves share the chip with the next frame's first.
- * Telling each context n lets RT_SCHED_AUTO pick the serial schedule for
- * launches of >= 32 pixels per lane at depth >= 7 (whole frames; scenes in
- * LDS without CSG), whose tail the overlap then hides. Default 1. Takes effect at once. No reference
+ * Telling each context n lets RT_SCHED_AUTO trade per-pixel latency for
+ * fewer idle lanes where the overlap hides the longer tail (scenes in LDS
+ * without CSG): serial samples instead of quads for launches of >= 32 pixels
+ * per lane at depth >= 7, and with the specialised kernel pixel pairs for
+ * branching scenes at 8-16 pixels per lane (depth < 7) or >= 16 (depth >= 7). Default 1. Takes effect at once. No reference
  * counterpart (Render is one synchronous frame, raytracer.go:589). */
 int rt_set_frames_in_flight(rt_context *ctx, int n);
 

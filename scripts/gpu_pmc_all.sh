@@ -5,8 +5,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for c in ${1:-c3 c3cone c4 c4csg c5}; do
-  # the schedule the in-flight bench picks (C4 whole frames: serial), one dispatch at a time
-  args=""; [ $c = c4 ] && args="--schedule pixel"
+  # the schedule the in-flight bench picks (C4 whole frames: pixel pairs), one dispatch at a time
+  args=""; [ $c = c4 ] && args="--schedule pairs"
   PMC_BENCH_ARGS="$args" bash scripts/gpu_pmc.sh $c > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 gpurun_out/pmc_$c.log; exit 1; }
   echo "== $c"; tail -2 gpurun_out/pmc_$c.log
 done

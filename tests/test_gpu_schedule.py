@@ -53,6 +53,7 @@ CASES = {
     "c3_small": lambda: rt.configs.c3(width=96, height=56),
     "canned_small": lambda: rt.configs.canned(width=64, height=40),
     "c4csg_small": lambda: rt.configs.c4csg(width=64, height=48),
+    "c3_ragged": lambda: rt.configs.c3(width=53, height=29),  # partial tiles and half tiles
 }
 
 
@@ -68,7 +69,9 @@ def test_tile_order_and_sharing_match_oracle(ctxs, case):
         try:
             for order in (True, False):
                 c.set_tile_order(order)
-                for mode in (rt.abi.RT_SCHED_PIXEL, rt.abi.RT_SCHED_QUADS):
+                # pairs: samples 0-1 / 2-3 in two lanes (specialised kernel;
+                # the generic and the work-sharing kernels run quads for it)
+                for mode in (rt.abi.RT_SCHED_PIXEL, rt.abi.RT_SCHED_QUADS, rt.abi.RT_SCHED_PAIRS):
                     c.set_schedule(mode)
                     img, st = render(c, packed)
                     what = "%s order=%s schedule=%d" % (case, order, mode)
@@ -97,11 +100,14 @@ def test_cost_estimate_leaves_counters_alone(ctxs):
     assert st.as_dict() == ost.as_dict()
 
 
-def test_interleaved_shares_with_order_match_full_frame(ctxs):
+@pytest.mark.parametrize("which", ["share", "pairs"])
+def test_interleaved_shares_with_order_match_full_frame(ctxs, which):
     """Strong-scaling shares (tile rows r, r + N, ...) each get their own
-    tile order; gathered, they are the oracle's frame."""
+    tile order; gathered, they are the oracle's frame (with work sharing, and
+    in the pixel-pairs schedule)."""
     import torch
-    s = ctxs[2]  # with work sharing
+    s = ctxs[2] if which == "share" else ctxs[1]
+    s.set_schedule(rt.abi.RT_SCHED_PAIRS if which == "pairs" else rt.abi.RT_SCHED_AUTO)
     args = rt.configs.c4(width=160, height=96)
     packed = rt.scene.convert(args)
     ref, ost = oracle_bind.render_rows(packed)
@@ -116,7 +122,8 @@ def test_interleaved_shares_with_order_match_full_frame(ctxs):
     torch.cuda.synchronize()
     img = rt.dist.deinterleave(slabs, packed.height).cpu().numpy()
     st = s.read_stats(reset=True)
-    assert_same(img, ref, "interleaved shares")
+    s.set_schedule(rt.abi.RT_SCHED_AUTO)
+    assert_same(img, ref, "interleaved shares (%s)" % which)
     assert st.as_dict() == ost.as_dict()
 
 
