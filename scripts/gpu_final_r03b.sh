@@ -10,7 +10,7 @@ for c in ${SWEEP_CFGS:-c1 c2 canned c3 c3cone c4 c4csg c5}; do
   timeout -k 10 400 python3 bench.py --config $c --steps $steps --warmup 1 --companion off > $O/sweep/$c.json 2> $O/sweep/$c.err || { echo "bench $c failed"; tail -5 $O/sweep/$c.err; exit 1; }
   echo "$c $(python3 -c "import json;d=json.load(open('$O/sweep/$c.json'));print(d['ms_per_step'], d['value'], d['roofline'].get('frac'), d['roofline'].get('executed_frac'))")"
 done
-for c in ${STRONG_CFGS:-c3 c3cone c4 c2}; do
+for c in ${STRONG_CFGS-c3 c3cone c4 c2}; do
   STRONG_WORLDS=1,2,4,8 timeout -k 10 300 python3 scripts/strong_emul.py $c 10 > $O/strong/$c.json 2> $O/strong/$c.err || { tail -5 $O/strong/$c.err; exit 1; }
   cat $O/strong/$c.json
 done

@@ -170,3 +170,31 @@ def test_frames_in_flight_hint_keeps_bytes_and_counters(specialize):
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("cfg,world", [("c3", 4), ("c4", 2)])
+def test_frames_in_flight_shares_keep_bytes_and_counters(cfg, world):
+    """Strong-scaling shares where the in-flight automatic schedule picks pixel
+    pairs (C3 over 4 ranks: 10 pixels per lane; C4 over 2: 21) equal the
+    default schedule's shares (quads) byte for byte and counter for counter."""
+    import torch
+    packed = rt.scene.convert(getattr(rt.configs, cfg)())
+    a = rt.RenderContext(0, specialize=True)
+    b = rt.RenderContext(0, specialize=True)
+    try:
+        b.set_frames_in_flight(2)
+        nt, K = rt.dist.tile_rows(packed.height, world)
+        n = max(0, min(K, (nt + world - 1) // world))  # rank 0's tile rows
+        outs = []
+        for c in (a, b):
+            c.set_scene(packed)
+            c.read_stats(reset=True)
+            buf = torch.zeros((n * 8, packed.width, 4), dtype=torch.uint8, device="cuda:0")
+            c.render_tile_rows_async(0, world, n, buf)
+            torch.cuda.synchronize()
+            outs.append((buf.cpu().numpy(), c.read_stats(reset=True).as_dict()))
+        assert_same(outs[1][0], outs[0][0], "%s rank 0 of %d: pairs vs quads" % (cfg, world))
+        assert outs[1][1] == outs[0][1]
+    finally:
+        a.close()
+        b.close()
