@@ -10,7 +10,7 @@ ROWS=${2:-2048:2304}
 O=gpurun_out/brute_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-B="python3 bench.py --config c5 --accel none --rows $ROWS --steps 1 --warmup 1 --cpu-baseline off"
+B="python3 bench.py --config c5 --accel none --rows $ROWS --steps 1 --warmup 1 --inflight 1 --cpu-baseline off"
 timeout -k 10 300 $B > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
 cat $O/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ks -o ks --output-format csv -- $B > /dev/null 2>&1 || { echo "ks failed"; exit 1; }
