@@ -307,7 +307,7 @@ __device__ __noinline__ double go_exp_amd64(double x, bool fma) {
   for (int i = 0; i < 4; i++) y = y * (y + T2);
   y = y + T1;
   int b = e + 0x3FF;
-  if (b < 0) {
+  if (b <= 0) {  // denormal (exp_amd64.s: JLE after the bias add)
     if (b < -52) return 0.0;
     b += 0x3FE;
     y = y * __longlong_as_double((long long)((uint64_t)(uint32_t)b << 52));

@@ -39,6 +39,8 @@
 #include <chrono>
 #include <functional>
 #include <cmath>
+#include <set>
+#include <thread>
 #include <array>
 #include <cstdio>
 #include <utility>
@@ -259,9 +261,25 @@ struct DevScene {
   int light_mask = 0;  // bit k: the scene has lights of kind k (RT_LIGHT_*)
   bool branching = false;  // some material is reflective and transparent, or a surface program may make one
   int leaf_kind_mask = 0;  // bit k: some CSG leaf has kind k
-  size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0;
+  size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0, off_arec = 0;
   int nruns = 0;
 };
+
+// A sphere whose WorldToObject is a scale + translation (rt_render.h
+// AXIS_REC): off-diagonal entries +-0, diagonal magnitudes in [2^-100, 2^100],
+// translations finite and non-zero. Its rayToObjectSpace (vec.go:298-313) then
+// equals the diagonal form bit for bit on rays that axis_ray_ok accepts.
+bool axis_sphere(const double* m) {
+  for (int q : {1, 2, 4, 6, 8, 9})
+    if (m[q] != 0.0) return false;
+  for (int q : {0, 5, 10}) {
+    const double a = std::fabs(m[q]);
+    if (!(a >= 0x1p-100 && a <= 0x1p100)) return false;
+  }
+  for (int q : {3, 7, 11})
+    if (!std::isfinite(m[q]) || m[q] == 0.0) return false;
+  return true;
+}
 
 #ifndef RT_BVH_SAH
 #define RT_BVH_SAH 1  // binned-SAH splits (median split when degenerate)
@@ -514,6 +532,8 @@ struct rt_context {
   // scene specialisation (rt_set_specialize)
   bool specialize = false;
   int accel = RT_ACCEL_BVH | RT_ACCEL_CULL;  // rt_set_accel
+  bool spec_async = false;          // rt_set_specialize(RT_SPECIALIZE_ASYNC): compile in the background
+  bool spec_waiting = false;        // ... and the current scene's kernel is still compiling
   hipFunction_t spec_fn = nullptr;  // specialised kernel of the current scene, if any
   hipFunction_t spec_alt_fn[3] = {nullptr, nullptr, nullptr};  // ... for the other pixel schedules (spec_for)
   SpecKey spec_key;                     // what spec_fn was compiled for
@@ -596,6 +616,23 @@ std::mutex g_spec_mu;
 Rtc g_rtc;
 std::map<std::string, SpecCode> g_spec_code;
 std::map<std::pair<int, std::string>, hipFunction_t> g_spec_fn;
+// Background compiles (RT_SPECIALIZE_ASYNC): keys in progress or failed, and
+// the threads, joined at exit (declared after the caches above, so destroyed
+// before them).
+std::mutex g_bg_mu;
+std::set<std::string> g_spec_busy, g_spec_failed;
+std::vector<std::thread> g_bg_threads;
+struct BgJoin {
+  ~BgJoin() {
+    std::vector<std::thread> t;
+    {
+      std::lock_guard<std::mutex> l(g_bg_mu);
+      t.swap(g_bg_threads);
+    }
+    for (auto& x : t)
+      if (x.joinable()) x.join();
+  }
+} g_bg_join;
 
 // Caller holds g_spec_mu.
 bool rtc_load() {
@@ -888,19 +925,64 @@ int spec_build(int device, const SpecKey& sk, hipFunction_t* fn, double* ms) {
   return RT_OK;
 }
 
+// Start compiling `sk` on a background thread (no-op if it is compiling,
+// compiled or failed before).
+void spec_compile_bg(const SpecKey& sk) {
+  const std::string key = sk.str();
+  std::lock_guard<std::mutex> l(g_bg_mu);
+  if (g_spec_busy.count(key) || g_spec_failed.count(key)) return;
+  g_spec_busy.insert(key);
+  g_bg_threads.emplace_back([sk, key] {
+    double ms = 0;
+    int rc;
+    {
+      std::lock_guard<std::mutex> lock(g_spec_mu);
+      rc = spec_compile(sk, &ms);
+    }
+    std::lock_guard<std::mutex> l2(g_bg_mu);
+    g_spec_busy.erase(key);
+    if (rc != RT_OK) g_spec_failed.insert(key);
+  });
+}
+
+// RT_SPECIALIZE_ASYNC: point c->spec_fn at the current scene's specialised
+// kernel once its background compile is done (never blocks on a compile).
+void spec_poll(rt_context* c) {
+  std::unique_lock<std::mutex> lock(g_spec_mu, std::try_to_lock);
+  if (!lock.owns_lock()) return;  // a compile is running
+  const std::string key = c->spec_key.str();
+  if (g_spec_code.count(key)) {
+    c->spec_waiting = false;
+    double ms = 0;
+    if (spec_build(c->device, c->spec_key, &c->spec_fn, &ms) != RT_OK) c->spec_fn = nullptr;
+    return;
+  }
+  lock.unlock();
+  std::lock_guard<std::mutex> l(g_bg_mu);
+  if (g_spec_failed.count(key)) c->spec_waiting = false;  // stays generic
+}
+
 // Point c->spec_fn at the specialised kernel of the current scene (or clear it).
 int spec_prepare(rt_context* c) {
   c->spec_fn = nullptr;
   c->spec_ms = 0;
+  c->spec_waiting = false;
   if (!c->specialize || !c->has_scene) return RT_OK;
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
   sk.quads = pick_schedule(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus, c->inflight, true);
-  if (sk.share && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the board assumes one owner lane per pixel
   sk.share = c->share_on ? 1 : 0;
+  if (sk.share && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the board assumes one owner lane per pixel
   c->spec_key = sk;
   for (auto& f : c->spec_alt_fn) f = nullptr;
+  if (c->spec_async) {
+    // the generic kernel until the background compile is done (spec_poll)
+    c->spec_waiting = true;
+    spec_poll(c);
+    if (c->spec_waiting) spec_compile_bg(sk);
+    return RT_OK;
+  }
   std::lock_guard<std::mutex> lock(g_spec_mu);
   return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
 }
@@ -911,6 +993,22 @@ int spec_for(rt_context* c, int sch, hipFunction_t* fn) {
   if (c->spec_fn && c->spec_key.share && sch == SCH_PAIRS) sch = SCH_QUADS;
   if (!c->spec_fn || c->spec_key.quads == sch) {
     *fn = c->spec_fn;
+    return RT_OK;
+  }
+  if (c->spec_async) {  // another schedule: generic until its compile is done
+    SpecKey sk = c->spec_key;
+    sk.quads = sch;
+    std::unique_lock<std::mutex> lock(g_spec_mu, std::try_to_lock);
+    if (lock.owns_lock() && g_spec_code.count(sk.str())) {
+      double ms = 0;
+      int rc = spec_build(c->device, sk, &c->spec_alt_fn[sch], &ms);
+      if (rc != RT_OK) return rc;
+      *fn = c->spec_alt_fn[sch];
+      return RT_OK;
+    }
+    if (lock.owns_lock()) lock.unlock();
+    spec_compile_bg(sk);
+    *fn = nullptr;
     return RT_OK;
   }
   if (!c->spec_alt_fn[sch]) {
@@ -955,7 +1053,9 @@ int rt_set_frames_in_flight(rt_context* c, int n) {
 
 int rt_set_specialize(rt_context* c, int enable) {
   if (!c) return fail(RT_E_INVALID, "rt_set_specialize: NULL context");
+  if (enable < 0 || enable > RT_SPECIALIZE_ASYNC) return fail(RT_E_INVALID, "rt_set_specialize: unknown mode");
   c->specialize = enable != 0;
+  c->spec_async = enable == RT_SPECIALIZE_ASYNC;
   return spec_prepare(c);
 }
 
@@ -1487,16 +1587,34 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     s.off_bobj = (b.nodes.size() * sizeof(float) + 15) & ~(size_t)15;
     s.off_planes = s.off_bobj + ((b.leaf_geo.size() * sizeof(double) + 15) & ~(size_t)15);
     // maximal runs of consecutive top-level objects of one kind (brute-force
-    // loops over global linear scenes: first, count, kind, 0)
+    // loops over global linear scenes: first, count, kind, axis), spheres split
+    // further into scale + translation runs (axis = 1: their compact records
+    // AXIS_REC doubles each, m0 m3 m5 m7 m10 m11, at off_arec by object index)
     std::vector<int> runs;
+    std::vector<double> arec;
     for (int i = 0; i < s.nobj; i++) {
-      if (runs.empty() || runs[runs.size() - 2] != kind[i]) runs.insert(runs.end(), {i, 0, kind[i], 0});
+      const int ax = kind[i] == RT_SPHERE && axis_sphere(&geo[(size_t)i * GEO]) ? 1 : 0;
+      if (ax && arec.empty()) arec.assign((size_t)s.nobj * AXIS_REC, 0.0);
+      if (ax) {
+        const double* m = &geo[(size_t)i * GEO];
+        double* a = &arec[(size_t)i * AXIS_REC];
+        a[0] = m[0];
+        a[1] = m[3];
+        a[2] = m[5];
+        a[3] = m[7];
+        a[4] = m[10];
+        a[5] = m[11];
+      }
+      if (runs.empty() || runs[runs.size() - 2] != kind[i] || runs[runs.size() - 1] != ax)
+        runs.insert(runs.end(), {i, 0, kind[i], ax});
       runs[runs.size() - 3]++;
     }
     s.nruns = (int)runs.size() / 4;
     s.off_runs = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
-    std::vector<char> acc(s.off_runs + std::max<size_t>(1, runs.size()) * sizeof(int), 0);
+    s.off_arec = (s.off_runs + std::max<size_t>(1, runs.size()) * sizeof(int) + 63) & ~(size_t)63;
+    std::vector<char> acc(s.off_arec + std::max<size_t>(1, arec.size()) * sizeof(double), 0);
     if (!runs.empty()) std::memcpy(acc.data() + s.off_runs, runs.data(), runs.size() * sizeof(int));
+    if (!arec.empty()) std::memcpy(acc.data() + s.off_arec, arec.data(), arec.size() * sizeof(double));
     if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
     if (!b.leaf_geo.empty())
       std::memcpy(acc.data() + s.off_bobj, b.leaf_geo.data(), b.leaf_geo.size() * sizeof(double));
@@ -1629,6 +1747,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
   // loads instead: no stream buffers)
   // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)
+  if (c->spec_waiting && !est) spec_poll(c);  // RT_SPECIALIZE_ASYNC: its compile may be done now
   static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
@@ -1762,6 +1881,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.cnt_off = cnt_off;
   P.runs = reinterpret_cast<const int*>(s.accel + s.off_runs);
   P.nruns = s.nruns;
+  P.arec = reinterpret_cast<const double*>(s.accel + s.off_arec);
   if (s.use_bvh) {
     P.bvh_nodes = reinterpret_cast<const float*>(s.accel + s.off_nodes);
     P.bvh_geo = reinterpret_cast<const double*>(s.accel + s.off_bobj);
@@ -1930,8 +2050,8 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
     unsigned long long tot = 0;
     for (int k = 0; k < N_PHASE; k++) tot += ph[k];
     if (tot) {
-      static const char* nm[N_PHASE] = {"refill", "trace_loop", "trace_unwind", "shade_surface",
-                                        "shadow_loops", "lighting", "material", "shade_unwind"};
+      static const char* nm[N_PHASE] = {"refill", "gen", "trace_loop", "trace_unwind", "shade_surface",
+                                        "light_dirs", "shadow_loops", "lighting", "material", "shade_unwind"};
       fprintf(stderr, "[phase]");
       for (int k = 0; k < N_PHASE; k++) fprintf(stderr, " %s=%.3f", nm[k], (double)ph[k] / (double)tot);
       fprintf(stderr, " total_wave_cycles=%.4g\n", (double)tot);
@@ -2049,29 +2169,49 @@ int rt_debug_run_surface(rt_context* c, int program, int n, const long long* fac
 
 int rt_render(const rt_scene* scene, uint8_t* rgba_out, rt_stats* stats) {
   if (!scene || !rgba_out) return fail(RT_E_INVALID, "rt_render: NULL argument");
+  // one context and one device frame buffer per device, kept between calls
+  // (the reference's Render allocates its image per call, raytracer.go:590)
+  struct Slot {
+    rt_context* c = nullptr;
+    void* buf = nullptr;
+    size_t bytes = 0;
+  };
   static std::mutex mu;
-  static std::vector<rt_context*> cache;
+  static std::vector<Slot> cache;
   std::lock_guard<std::mutex> lock(mu);
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
-  if ((int)cache.size() <= dev) cache.resize(dev + 1, nullptr);
-  if (!cache[dev]) {
-    int rc = rt_create(dev, &cache[dev]);
+  if ((int)cache.size() <= dev) cache.resize(dev + 1);
+  Slot& sl = cache[dev];
+  if (!sl.c) {
+    int rc = rt_create(dev, &sl.c);
     if (rc != RT_OK) return rc;
+    const char* e = getenv("RT_RENDER_SPECIALIZE");
+    const int mode = e ? atoi(e) : RT_SPECIALIZE_ASYNC;
+    if (mode) {
+      rc = rt_set_specialize(sl.c, mode == 1 ? 1 : RT_SPECIALIZE_ASYNC);
+      if (rc != RT_OK) return rc;
+    }
   }
-  rt_context* c = cache[dev];
+  rt_context* c = sl.c;
+  if (scene->width <= 1 || scene->height <= 1) return fail(RT_E_INVALID, "rt_set_scene: width/height must be > 1");
+  const size_t bytes = (size_t)scene->width * scene->height * 4;
+  if (bytes > sl.bytes) {
+    (void)hipFree(sl.buf);
+    sl.buf = nullptr;
+    sl.bytes = 0;
+    DeviceGuard guard(dev);
+    if (hipMalloc(&sl.buf, bytes) != hipSuccess) return fail(RT_E_NOMEM, "rt_render: frame buffer");
+    sl.bytes = bytes;
+  }
   int rc = rt_set_scene(c, scene);
   if (rc != RT_OK) return rc;
-  size_t bytes = (size_t)scene->width * scene->height * 4;
-  void* d = nullptr;
-  HIP_TRY(hipMalloc(&d, bytes));
   rt_stats tmp;
   rc = rt_read_stats(c, nullptr, 1, &tmp);
-  if (rc == RT_OK) rc = rt_render_rows_async(c, 0, scene->height, d, nullptr);
-  if (rc == RT_OK && hipMemcpy(rgba_out, d, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+  if (rc == RT_OK) rc = rt_render_rows_async(c, 0, scene->height, sl.buf, nullptr);
+  if (rc == RT_OK && hipMemcpy(rgba_out, sl.buf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(RT_E_DEVICE, "rt_render: copy back failed");
   if (rc == RT_OK && stats) rc = rt_read_stats(c, nullptr, 1, stats);
-  (void)hipFree(d);
   return rc;
 }
 

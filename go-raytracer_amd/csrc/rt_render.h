@@ -72,6 +72,17 @@
 #ifndef RT_BRANCHFREE
 #define RT_BRANCHFREE 0  // straight-line Intersect routines: measured -35M scalar, +45M vector instructions on C3, no faster
 #endif
+#ifndef RT_CULL_NOBRANCH
+#define RT_CULL_NOBRANCH 1  // cull tests combined without short-circuit branches (see CULL_AND)
+#endif
+// a && b for the pure, cheap lane predicates of the culls: evaluated on every
+// lane without a branch (no exec-mask save/restore, and the result stays a
+// lane mask for the wave's any-lane test instead of being rematerialised)
+#if RT_CULL_NOBRANCH
+#define CULL_AND(a, b) (bool)((int)(bool)(a) & (int)(bool)(b))
+#else
+#define CULL_AND(a, b) ((a) && (b))
+#endif
 #ifndef RT_CUBE_FAST
 #define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
 #endif
@@ -165,7 +176,7 @@ enum { QSET = QHEADS * QSTRIDE /* u32 per launch set of heads */,
 #endif
 enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
-       ST_PHASE = 16, N_PHASE = 8, ST_BVHDIAG = 24, ST_EXDIAG = 32, ST_SHDIAG = 48, ST_WATCHDOG = 63,
+       ST_PHASE = 16, N_PHASE = 10, ST_BVHDIAG = 26, ST_EXDIAG = 34, ST_SHDIAG = 48, ST_WATCHDOG = 63,
        STATS_PART = 16 /* u64 per workgroup record: one 128-B line */ };
 // Diagnostic build (RT_PHASE_TIMING): work-sharing events, ST_SHDIAG + k:
 // 0 samples posted, 1 subtrees posted, 2 claims, 3 reclaims, 4 waits, 5 rounds
@@ -226,6 +237,7 @@ struct Params {
   // [nruns][4] = first index, count, kind, 0 (brute-force scalar-load loops)
   const int* runs;
   int nruns;
+  const double* arec;  // [nobj][AXIS_REC] compact records of axis-aligned spheres (runs with axis = 1)
   int cnt_off;    // LDS byte offset of the event counters (CNT_BYTES)
   int kind_mask;  // bit k: the scene has objects of kind k
   int board_off;  // LDS byte offset of the work-sharing board (RT_SHARE)
@@ -259,27 +271,59 @@ struct Ray {
 
 // rayToObjectSpace (raytracer.go:51-56) with prim.Mat4.MulPoint/MulDir
 // (vec.go:298-313): m points at the 3x4 affine rows.
+__device__ __forceinline__ d3 to_obj_o(const double* m, d3 o) {  // MulPoint (vec.go:298-304)
+  return mk(m[0] * o.x + m[1] * o.y + m[2] * o.z + m[3], m[4] * o.x + m[5] * o.y + m[6] * o.z + m[7],
+            m[8] * o.x + m[9] * o.y + m[10] * o.z + m[11]);
+}
+__device__ __forceinline__ d3 to_obj_d(const double* m, d3 d) {  // MulDir (vec.go:307-313)
+  return mk(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
+            m[8] * d.x + m[9] * d.y + m[10] * d.z);
+}
 __device__ __forceinline__ Ray to_obj(const double* m, const Ray& r) {
   Ray l;
-  l.o = mk(m[0] * r.o.x + m[1] * r.o.y + m[2] * r.o.z + m[3], m[4] * r.o.x + m[5] * r.o.y + m[6] * r.o.z + m[7],
-           m[8] * r.o.x + m[9] * r.o.y + m[10] * r.o.z + m[11]);
-  l.d = mk(m[0] * r.d.x + m[1] * r.d.y + m[2] * r.d.z, m[4] * r.d.x + m[5] * r.d.y + m[6] * r.d.z,
-           m[8] * r.d.x + m[9] * r.d.y + m[10] * r.d.z);
+  l.o = to_obj_o(m, r.o);
+  l.d = to_obj_d(m, r.d);
   return l;
 }
+// rayToObjectSpace for a scale + translation (host: axis_sphere; a = m0 m3
+// m5 m7 m10 m11): o' = (m0*ox + m3, m5*oy + m7, m10*oz + m11), d' = (m0*dx,
+// m5*dy, m10*dz). Bit-identical to MulPoint / MulDir (vec.go:298-313) when
+// axis_ray_ok(o, d): the off-diagonal entries are +-0, so with finite ray
+// components their products are +-0; a direction component d != 0 with
+// |d| in [2^-900, 2^900) and |m0| in [2^-100, 2^100] gives a normal non-zero
+// product p = m0*d, and p + (+-0) + (+-0) = p exactly, whatever the zeros'
+// signs; an origin component o is either such a number (then the row is
+// p + m3 in both forms) or +-0, when the full row is a sum of signed zeros
+// plus m3 != 0, i.e. m3, as is +-0 + m3. Where some lane's ray fails the
+// test the wave takes the full form (wave-uniform choice).
+__device__ __forceinline__ bool ax_mag(double x, bool zero_ok) {
+  const uint32_t e = ((uint32_t)__double2hiint(x) >> 20) & 0x7ffu;  // biased exponent
+  return e - 123u < 1800u || (zero_ok && x == 0.0);                  // |x| in [2^-900, 2^900)
+}
+__device__ __forceinline__ bool axis_o_ok(d3 o) { return ax_mag(o.x, true) && ax_mag(o.y, true) && ax_mag(o.z, true); }
+__device__ __forceinline__ bool axis_d_ok(d3 d) { return ax_mag(d.x, false) && ax_mag(d.y, false) && ax_mag(d.z, false); }
+__device__ __forceinline__ d3 axis_o(const double* a, d3 o) {
+  return mk(a[0] * o.x + a[1], a[2] * o.y + a[3], a[4] * o.z + a[5]);
+}
+__device__ __forceinline__ d3 axis_d(const double* a, d3 d) { return mk(a[0] * d.x, a[2] * d.y, a[4] * d.z); }
 
 // Object records read through the constant address space: a wave-uniform
 // index then compiles to scalar loads (s_load_dwordx16 + x8 for the 12
 // WorldToObject doubles), which land in SGPRs and feed the FP64 VALU ops as
 // their scalar operand -- no LDS or vector-memory bandwidth per object.
 typedef const __attribute__((address_space(4))) double* cdptr;
-struct Rec12 {
-  double m[12];
+template <int N>
+struct RecN {
+  double m[N];
 };
-__device__ __forceinline__ Rec12 ld_rec12(cdptr p) {
-  Rec12 r;
+typedef RecN<12> Rec12;  // WorldToObject rows (geo records, GEO doubles apart)
+typedef RecN<6> Rec6;    // axis-aligned sphere: m0 m3 m5 m7 m10 m11 (arec, AXIS_REC doubles apart)
+enum { AXIS_REC = 8 };
+template <int N>
+__device__ __forceinline__ RecN<N> ld_rec(cdptr p) {
+  RecN<N> r;
 #pragma unroll
-  for (int q = 0; q < 12; q++) r.m[q] = p[q];
+  for (int q = 0; q < N; q++) r.m[q] = p[q];
   return r;
 }
 // Index of the next record to prefetch, made to depend on the current record
@@ -287,24 +331,26 @@ __device__ __forceinline__ Rec12 ld_rec12(cdptr p) {
 // only wait the compiler can emit is lgkmcnt(0); this places that wait before
 // the next record's loads are issued instead of right after them, so they
 // stay in flight while the current record is tested.
-__device__ __forceinline__ cdptr after_rec(cdptr next, const Rec12& cur) {
+template <int N>
+__device__ __forceinline__ cdptr after_rec(cdptr next, const RecN<N>& cur) {
   asm volatile("" : "+s"(next) : "s"(cur.m[0]));
   return next;
 }
 // body(i, rec) for the objects i = r0 .. r0 + rn - 1 in index order, records
-// read with scalar loads, the next record in flight while one is tested. Two
-// register sets alternate (no copies between iterations). With CHECK > 0
-// (even), stop() -- wave-uniform -- is asked every CHECK objects.
-template <int CHECK, typename Body, typename Stop>
+// (N doubles, STRIDE apart) read with scalar loads, the next record in flight
+// while one is tested. Two register sets alternate (no copies between
+// iterations). With CHECK > 0 (even), stop() -- wave-uniform -- is asked
+// every CHECK objects.
+template <int CHECK, int N = 12, int STRIDE = 16, typename Body, typename Stop>
 __device__ __forceinline__ void scan_records(cdptr base, int r0, int rn, Body&& body, Stop&& stop) {
-  cdptr p = base + (size_t)r0 * 16;  // GEO doubles per record
-  Rec12 A = ld_rec12(p);
+  cdptr p = base + (size_t)r0 * STRIDE;
+  RecN<N> A = ld_rec<N>(p);
   int j = 0;
-  for (; j + 2 <= rn; j += 2, p += 2 * 16) {
+  for (; j + 2 <= rn; j += 2, p += 2 * STRIDE) {
     if (CHECK > 0 && j > 0 && (j % CHECK) == 0 && stop()) return;
-    const Rec12 B = ld_rec12(after_rec(p + 16, A));
+    const RecN<N> B = ld_rec<N>(after_rec(p + STRIDE, A));
     body(r0 + j, A);
-    A = ld_rec12(after_rec(j + 2 < rn ? p + 2 * 16 : p + 16, B));
+    A = ld_rec<N>(after_rec(j + 2 < rn ? p + 2 * STRIDE : p + STRIDE, B));
     body(r0 + j + 1, B);
   }
   if (j < rn) {
@@ -326,10 +372,12 @@ __device__ __forceinline__ bool t_nonpos(double num, double den) {
 }
 
 // Sphere.Intersect (raytracer.go:58-104): unit sphere, near root only.
-__device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
+// c = O.O - 1 depends on the ray origin only (shared by the shadow rays of a
+// hit, see shadow_sweep); sphere_hit forms it.
+__device__ __forceinline__ double sphere_c(d3 o) { return dot(o, o) - 1.0; }
+__device__ __forceinline__ bool sphere_hit_c(const Ray& l, double c, double& t) {
   double a = dot(l.d, l.d);
   double hb = dot(l.o, l.d);
-  double c = dot(l.o, l.o) - 1.0;
   double disc = hb * hb - a * c;
   if (disc < 0.0) return false;
   double sq = gsqrt(disc);
@@ -342,17 +390,22 @@ __device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) {
   }
   return false;
 }
+__device__ __forceinline__ bool sphere_hit(const Ray& l, double& t) { return sphere_hit_c(l, sphere_c(l.o), t); }
 
-// Plane.Intersect (raytracer.go:164-180) on an object-space ray.
-__device__ __forceinline__ bool plane_hit(const Ray& l, d3 n, double pd, double& t) {
+// Plane.Intersect (raytracer.go:164-180) on an object-space ray; no = n.O
+// (origin only).
+__device__ __forceinline__ bool plane_hit_c(const Ray& l, d3 n, double pd, double no, double& t) {
   double denom = dot(n, l.d);
   if (__builtin_fabs(denom) < 1e-6) return false;
-  double num = -pd - dot(n, l.o);
+  double num = -pd - no;
   if (t_nonpos(num, denom)) return false;
   double tt = num / denom;
   if (tt <= 0.0) return false;
   t = tt;
   return true;
+}
+__device__ __forceinline__ bool plane_hit(const Ray& l, d3 n, double pd, double& t) {
+  return plane_hit_c(l, n, pd, dot(n, l.o), t);
 }
 
 // Cube.Intersect (raytracer.go:214-240) over prim.PlanesForUnitCube
@@ -425,18 +478,19 @@ __device__ __forceinline__ bool cube_hit(const Ray& l, double& t, int& face) {
 // is wave-uniform) keeps register pressure at the cylinder's. Every quantity
 // is formed in the oracle's op order: the cone's a, halfB, c0 append
 // "- dy*dy", "- oy*dy", "- oy*oy" where the cylinder has nothing / "- 1.0".
-__device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, bool cone) {
+// c0: the origin-only term (quadric_c0).
+__device__ __forceinline__ double quadric_c0(d3 o, bool cone) {
+  const double c0 = o.x * o.x + o.z * o.z;
+  return cone ? c0 - o.y * o.y : c0 - 1.0;
+}
+__device__ __forceinline__ bool quadric_hit_c(const Ray& l, double c0, double& t, int& face, bool cone) {
   double bestT = __builtin_inf();
   int bestFace = -1;
   double a = l.d.x * l.d.x + l.d.z * l.d.z;
   double hb = l.o.x * l.d.x + l.o.z * l.d.z;
-  double c0 = l.o.x * l.o.x + l.o.z * l.o.z;
   if (cone) {
     a = a - l.d.y * l.d.y;
     hb = hb - l.o.y * l.d.y;
-    c0 = c0 - l.o.y * l.o.y;
-  } else {
-    c0 = c0 - 1.0;
   }
   if (__builtin_fabs(a) > 1e-12) {  // cylinder: a >= 0, the reference's a > 1e-12
     double disc = hb * hb - a * c0;
@@ -497,6 +551,9 @@ __device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, 
   t = bestT;
   face = bestFace;
   return true;
+}
+__device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, bool cone) {
+  return quadric_hit_c(l, quadric_c0(l.o, cone), t, face, cone);
 }
 
 
@@ -600,7 +657,32 @@ __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r,
   return quadric_hit(l, t, face, spec_kind(RT_CONE) && (!spec_kind(RT_CYLINDER) || k == RT_CONE));
 }
 
-__device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(__ballot(b)); }
+// The origin-only term of kind k's Intersect for object-space origin o
+// (sphere c, cylinder / cone c0, plane n.O; cube: none).
+__device__ __forceinline__ double object_oc(int k, const double* g, d3 o) {
+  if (spec_kind(RT_SPHERE) && k == RT_SPHERE) return sphere_c(o);
+  if (spec_kind(RT_PLANE) && k == RT_PLANE) return dot(mk(g[12], g[13], g[14]), o);
+  if (spec_kind(RT_CYLINDER) && k == RT_CYLINDER) return quadric_c0(o, false);
+  if (spec_kind(RT_CONE) && k == RT_CONE) return quadric_c0(o, true);
+  return 0.0;
+}
+// object_hit on an object-space ray l whose origin term oc = object_oc(k, g,
+// l.o) is given: the same operations, so the same result.
+__device__ __forceinline__ bool object_hit_l(int k, const double* g, const Ray& l, double oc, double& t, int& face) {
+  face = 0;
+  if (spec_kind(RT_SPHERE) && k == RT_SPHERE) return sphere_hit_c(l, oc, t);
+  if (spec_kind(RT_PLANE) && k == RT_PLANE) return plane_hit_c(l, mk(g[12], g[13], g[14]), g[15], oc, t);
+  if (spec_kind(RT_CUBE) && k == RT_CUBE) return cube_hit(l, t, face);
+  if (!spec_kind(RT_CYLINDER) && !spec_kind(RT_CONE)) return false;
+  return quadric_hit_c(l, oc, t, face, spec_kind(RT_CONE) && (!spec_kind(RT_CYLINDER) || k == RT_CONE));
+}
+
+// Wave votes on a lane predicate, straight from its lane mask (HIP's
+// __any / __ballot take an int: the predicate is first rematerialised as 0/1
+// in a VGPR and compared again).
+__device__ __forceinline__ uint64_t wave_ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+__device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
+__device__ __forceinline__ uint64_t popc_ballot(bool b) { return (uint64_t)__popcll(wave_ballot(b)); }
 
 // Conservative FP32 test: can the segment o + t*d, 0 < t < tmax (d ~ unit)
 // come within the padded bounding sphere (centre c, radius^2 r2)? The exact
@@ -633,6 +715,25 @@ __device__ __forceinline__ bool may_hit_oc(float ox, float oy, float oz, float r
   float qx = __builtin_fmaf(-tc, d.x, ox), qy = __builtin_fmaf(-tc, d.y, oy), qz = __builtin_fmaf(-tc, d.z, oz);
   return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= r2;
 }
+// The culls with the lane's activity folded into the final compare (an
+// inactive lane compares against an unreachable bound), so the result is one
+// compare's lane mask: the wave's any-lane test reads it directly (a && of
+// two lane masks is rematerialised through a VGPR before a ballot).
+__device__ __forceinline__ bool may_hit_a(bool act, F3 o, F3 d, float tmax, const double* g, float slack) {
+  const float* b = reinterpret_cast<const float*>(g + 12);
+  float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
+  float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
+  tc = fminf(fmaxf(tc, 0.0f), tmax);
+  float qx = __builtin_fmaf(-tc, d.x, ox), qy = __builtin_fmaf(-tc, d.y, oy), qz = __builtin_fmaf(-tc, d.z, oz);
+  const float R = b[3] + slack;
+  return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= (act ? R * R : -1.0f);
+}
+__device__ __forceinline__ bool may_hit_oc_a(bool act, float ox, float oy, float oz, float r2, F3 d, float tmax) {
+  float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
+  tc = fminf(fmaxf(tc, 0.0f), tmax);
+  float qx = __builtin_fmaf(-tc, d.x, ox), qy = __builtin_fmaf(-tc, d.y, oy), qz = __builtin_fmaf(-tc, d.z, oz);
+  return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= (act ? r2 : -1.0f);
+}
 __device__ __forceinline__ float ray_slack(F3 o) {
   return 1e-5f * (1.0f + __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z));
 }
@@ -648,6 +749,19 @@ __device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax
   tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
   const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
   return tn <= tf && tf >= 0.0f && tn <= tmax;
+}
+// may_hit_box as one compare, the lane's activity folded in: for tmax >= 0,
+// tn <= tf && tf >= 0 && tn <= tmax  <=>  max(tn, 0) <= min(tf, tmax); an
+// inactive lane's bound is -1 (a NaN tn or tmax can only admit more nodes:
+// still conservative).
+__device__ __forceinline__ bool may_hit_box_a(bool act, F3 o, F3 id, float slack, float tmax, const float* nb,
+                                              float& tn) {
+  const float x0 = (nb[0] - slack - o.x) * id.x, x1 = (nb[3] + slack - o.x) * id.x;
+  const float y0 = (nb[1] - slack - o.y) * id.y, y1 = (nb[4] + slack - o.y) * id.y;
+  const float z0 = (nb[2] - slack - o.z) * id.z, z1 = (nb[5] + slack - o.z) * id.z;
+  tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+  return fmaxf(tn, 0.0f) <= fminf(tf, act ? tmax : -1.0f);
 }
 // Per-wave traversal stack in LDS: node refs and the lanes still active there.
 struct WaveStack {
@@ -1016,12 +1130,23 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
 // in FP32 and `false` needs them to agree in sign with a 1e-4 margin, so the
 // exact test misses (or cannot beat the current best). tmax >= 1e30 means no
 // bound: then f(0) and the slope must agree in sign (the root lies behind).
-__device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, const double* sh) {
+// The origin-only half (f(0) and its term scale), shared by the shadow rays
+// of one hit (shadow_sweep); may_hit_plane_d finishes the test.
+struct PlaneO {
+  float f0, a0;
+};
+__device__ __forceinline__ PlaneO may_hit_plane_o(F3 o, const double* sh) {
   const float* c = reinterpret_cast<const float*>(sh + 16);
-  const float f0 = __builtin_fmaf(c[0], o.x, __builtin_fmaf(c[1], o.y, __builtin_fmaf(c[2], o.z, c[3])));
+  PlaneO r;
+  r.f0 = __builtin_fmaf(c[0], o.x, __builtin_fmaf(c[1], o.y, __builtin_fmaf(c[2], o.z, c[3])));
+  r.a0 = __builtin_fmaf(c[4], __builtin_fabsf(o.x),
+                        __builtin_fmaf(c[5], __builtin_fabsf(o.y), __builtin_fmaf(c[6], __builtin_fabsf(o.z), c[7])));
+  return r;
+}
+__device__ __forceinline__ bool may_hit_plane_d(PlaneO po, F3 d, float tmax, const double* sh) {
+  const float* c = reinterpret_cast<const float*>(sh + 16);
+  const float f0 = po.f0, a0 = po.a0;
   const float sl = __builtin_fmaf(c[0], d.x, __builtin_fmaf(c[1], d.y, c[2] * d.z));
-  const float a0 = __builtin_fmaf(c[4], __builtin_fabsf(o.x),
-                                  __builtin_fmaf(c[5], __builtin_fabsf(o.y), __builtin_fmaf(c[6], __builtin_fabsf(o.z), c[7])));
   const float a1 = __builtin_fmaf(c[4], __builtin_fabsf(d.x), __builtin_fmaf(c[5], __builtin_fabsf(d.y), c[6] * __builtin_fabsf(d.z)));
   float f1, m0, m1;
   if (tmax >= 1e30f) {
@@ -1034,6 +1159,9 @@ __device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, const doub
     m1 = m0;
   }
   return !((f0 > m0 && f1 > m1) || (f0 < -m0 && f1 < -m1));
+}
+__device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, const double* sh) {
+  return may_hit_plane_d(may_hit_plane_o(o, sh), d, tmax, sh);
 }
 
 // Diagnostic build only (-DRT_PHASE_TIMING): wave cycles per phase, stamped
@@ -1064,7 +1192,7 @@ __device__ __forceinline__ uint64_t stamp() {
 #ifdef RT_EXACT_DIAG
 #define EXDIAG(k, sh, b)                                                                    \
   do {                                                                                      \
-    const uint64_t act_ = __ballot(1), m_ = __ballot(b);                                    \
+    const uint64_t act_ = wave_ballot(1), m_ = wave_ballot(b);                                    \
     if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1) {                          \
       atomicAdd(P.stats + ST_EXDIAG + 2 * (k) + (sh), (unsigned long long)__popcll(m_));    \
       atomicAdd(P.stats + ST_EXDIAG + 2 * RT_NUM_KINDS + (sh), 1ull);                       \
@@ -1544,14 +1672,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   auto cnt_kind = [&](int k, uint64_t v) { atomicAdd(&kcnt[k * WG + threadIdx.x], (unsigned long long)v); };
   // a unit event on the lanes where b holds (wave-uniform call)
   auto cnt_unit = [&](int k, bool b) {
-    const unsigned int n = (unsigned int)__popcll(__ballot(b));
+    const unsigned int n = (unsigned int)__popcll(wave_ballot(b));
     if (lane == 0 && n) atomicAdd(&cnt[k * WAVES_PER_WG + wave], (unsigned long long)n);
   };
   WaveStack bst;
   bst.mask = reinterpret_cast<uint64_t*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
   bst.ref = reinterpret_cast<int*>(smem + P.bvh_stack_off + WAVES_PER_WG * BVH_STACK * 8) + (threadIdx.x >> 6) * BVH_STACK;
 #ifdef RT_PHASE_TIMING
-  uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph_acc[N_PHASE] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t bd_tnodes = 0, bd_snodes = 0, bd_tleaf = 0, bd_sleaf = 0, bd_trays = 0, bd_srays = 0;
 #ifdef RT_COST_MAP
   uint32_t lane_cost = 0;  // node visits charged to this lane's pixel (diagnostic)
@@ -1647,7 +1775,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // tracing its next ray (pending refraction child / next sample), waiting
   // for a helper (S_WAIT) or idle.
   auto unwind = [&](bool have_res, d3 res, bool pf_valid, long long pf_packed, d3 pf_lw, double pf_kr) {
-    while (__any(have_res)) {
+    while (wave_any(have_res)) {
       if (have_res) {
         if (sp == 0) {
           if constexpr (QD) {
@@ -1761,11 +1889,11 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     // ---- serial samples: a lane that finished a sample goes on with the next
     // one (or hands a claimed sample's colour to its owner) ----
     if constexpr (!QD) {
-      if (__any(state == S_ADV)) {
+      if (wave_any(state == S_ADV)) {
         // a lane about to finish a pixel while it still holds one: every
         // held pixel goes out in one store first (with sharing a lane may also
         // finish by taking helpers' colours, so any advancing holder flushes)
-        if (RT_PIX_BATCH && __any(state == S_ADV && held_px != ~0u && (RT_SHARE || (!PR && sample == 4)))) flush_pixels();
+        if (RT_PIX_BATCH && wave_any(state == S_ADV && held_px != ~0u && (RT_SHARE || (!PR && sample == 4)))) flush_pixels();
         if (state == S_ADV) {
           const uint32_t w = RT_SHARE ? Bd->lw[threadIdx.x] : 4u;
           if (RT_SHARE && __builtin_expect(lw_task(w) >= 0, 0)) {
@@ -1782,7 +1910,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     // colours in sample order (raytracer.go:651) and quantises
     // (raytracer.go:656, vec.go:104-107); the quad becomes idle ----
     if constexpr (QD) {
-      const uint64_t dn = __ballot(state == S_DONE);
+      const uint64_t dn = wave_ballot(state == S_DONE);
       const uint64_t qd = dn & (dn >> 1) & (dn >> 2) & (dn >> 3) & 0x1111111111111111ull;
       if (qd) {
         // running sum (((0 + s0) + s1) + s2) + s3, one neighbour's colour at a time
@@ -1792,7 +1920,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const int lk = (lane + k) & 63;
           sm = add(sm, mk(__shfl(sum.x, lk), __shfl(sum.y, lk), __shfl(sum.z, lk)));
         }
-        if (RT_PIX_BATCH && __any(((qd >> lane) & 1) && held_px != ~0u)) flush_pixels();
+        if (RT_PIX_BATCH && wave_any(((qd >> lane) & 1) && held_px != ~0u)) flush_pixels();
         if ((qd >> lane) & 1) {
           const d3 c = scale(sm, 1.0 / 4.0);
           const uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
@@ -1814,14 +1942,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     // neighbour's two colours (raytracer.go:651) -- and quantises
     // (raytracer.go:656, vec.go:104-107); the pair becomes idle ----
     if constexpr (PR) {
-      const uint64_t dn = __ballot(state == S_DONE);
+      const uint64_t dn = wave_ballot(state == S_DONE);
       const uint64_t pd = dn & (dn >> 1) & 0x5555555555555555ull;
       if (pd) {
         const int lb = (lane + 1) & 63;
         const d3 c2 = mk(__shfl(sum.x, lb), __shfl(sum.y, lb), __shfl(sum.z, lb));
         const d3 c3 = mk(__shfl(sum2.x, lb), __shfl(sum2.y, lb), __shfl(sum2.z, lb));
         const d3 sm = add(add(sum, c2), c3);
-        if (RT_PIX_BATCH && __any(((pd >> lane) & 1) && held_px != ~0u)) flush_pixels();
+        if (RT_PIX_BATCH && wave_any(((pd >> lane) & 1) && held_px != ~0u)) flush_pixels();
         if ((pd >> lane) & 1) {
           const d3 c = scale(sm, 1.0 / 4.0);
           const uint32_t r8 = go_f64_to_u32(c.x * 65535.0) >> 8;
@@ -1842,7 +1970,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     for (;;) {
       // with quads a pixel goes to a quad whose 4 lanes are all idle, sample k
       // to lane 4p+k; mask = the idle lanes / the idle quads' first lanes
-      const uint64_t il = __ballot(state == S_IDLE);
+      const uint64_t il = wave_ballot(state == S_IDLE);
       const uint64_t mask = QD   ? il & (il >> 1) & (il >> 2) & (il >> 3) & 0x1111111111111111ull
                             : PR ? il & (il >> 1) & 0x5555555555555555ull
                                  : il;
@@ -1949,7 +2077,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       // (a) owners whose helper delivered take the colour; it is propagated
       // by the TRACE pass's unwind (a posted sample is added in sample order
       // at sp == 0, a posted refraction child combined at its frame)
-      if (__builtin_expect(__any(state == S_WAIT), 0)) {
+      if (__builtin_expect(wave_any(state == S_WAIT), 0)) {
         if (state == S_WAIT && board_done(Bd, wait_slot())) state = S_RESUME;
       }
       // (b) owners post work they have not started, while drained waves of
@@ -1973,7 +2101,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             if ((f & (FL_HASR | FL_HAST | FL_STAGE | FL_FORKED)) == (FL_HASR | FL_HAST)) L = l;
           }
         const bool cand = cs || L >= 0;
-        const uint64_t cm = __ballot(cand);
+        const uint64_t cm = wave_ballot(cand);
         if (cm) {
           const uint32_t wf = (uint32_t)__builtin_amdgcn_readfirstlane(
               (int)__hip_atomic_load(&Bd->wfree[wave], __ATOMIC_RELAXED, RT_WG_SCOPE));
@@ -2016,7 +2144,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         }
       }
       // (c) idle lanes of a drained wave claim posted tasks
-      uint64_t il = exhausted ? __ballot(state == S_IDLE) : 0ull;
+      uint64_t il = exhausted ? wave_ballot(state == S_IDLE) : 0ull;
       if (__builtin_expect(il != 0, 0)) {
         const uint64_t pm0 = __hip_atomic_load(&Bd->post, __ATOMIC_RELAXED, RT_WG_SCOPE);
         const uint64_t pm = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(pm0 >> 32)) << 32) |
@@ -2051,7 +2179,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             }
             state = S_TRACE;
           }
-          il = __ballot(state == S_IDLE);
+          il = wave_ballot(state == S_IDLE);
         }
       }
       // (d) bookkeeping for the board: helpers available, waves still busy
@@ -2060,7 +2188,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if (lane == 0) __hip_atomic_fetch_add(&Bd->nidle, cur_idle - my_idle, __ATOMIC_RELAXED, RT_WG_SCOPE);
         my_idle = cur_idle;
       }
-      const bool busy = __any(state != S_IDLE);
+      const bool busy = wave_any(state != S_IDLE);
       if (busy != my_active) {
         if (lane == 0) __hip_atomic_fetch_add(&Bd->nactive, busy ? 1 : -1, __ATOMIC_RELAXED, RT_WG_SCOPE);
         my_active = busy;
@@ -2083,24 +2211,25 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         continue;
       }
       spins = 0;
-      if (__builtin_expect(!__any(state == S_TRACE || state == S_SHADE || state == S_RESUME), 0)) {  // only waiting (or quad-holding) lanes
+      if (__builtin_expect(!wave_any(state == S_TRACE || state == S_SHADE || state == S_RESUME), 0)) {  // only waiting (or quad-holding) lanes
         __builtin_amdgcn_s_sleep(RT_SHARE_SLEEP / 4);
         continue;
       }
     } else {
-      if (!__any(state != S_IDLE)) break;
+      if (!wave_any(state != S_IDLE)) break;
     }
+    PH_MARK(0);
     // ---- new sample rays for every lane that needs one, in one block ----
-    if (__any(need_gen)) {
+    if (wave_any(need_gen)) {
       if (need_gen) {
         gen_ray();
         need_gen = false;
       }
     }
-    PH_MARK(0);
+    PH_MARK(1);
 
     // ---- TRACE pass: closestHit over all objects (raytracer.go:469-483) ----
-    if (__any(state == S_TRACE || (RT_SHARE && state == S_RESUME))) {
+    if (wave_any(state == S_TRACE || (RT_SHARE && state == S_RESUME))) {
       const bool tr = state == S_TRACE;
       // Prefetch the parent frame: a ray that misses pops it right after
       // this pass, and the load latency hides under the object loop.
@@ -2130,9 +2259,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #if RT_CULL
         // an object entered beyond the lane's current best cannot win (strict <)
         const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
-        test = test && (k != RT_PLANE ? may_hit(of, df, tmax, g, slack)
-                                      : may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
-        if (!__any(test)) return;
+        test = k != RT_PLANE ? may_hit_a(test, of, df, tmax, g, slack)
+                             : CULL_AND(test, may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
+        if (!wave_any(test)) return;
 #endif
         EXDIAG(k, 0, test);
         if (test) {
@@ -2170,25 +2299,35 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           // lanes with a real root take the sqrt/division branch; index order,
           // strict < (closestHit, raytracer.go:469-483).
           const cdptr cgeo = (cdptr)S.geo;
+          auto tsphere = [&](int i, const Ray& l) {
+            const double a = dot(l.d, l.d);
+            const double hb = dot(l.o, l.d);
+            const double c = dot(l.o, l.o) - 1.0;
+            const double disc = hb * hb - a * c;
+            if (tr && !(disc < 0.0)) {
+              const double t0 = (-hb - gsqrt(disc)) / a;
+              if (t0 > 0.0 && (!found || t0 < best_t)) {
+                found = true;
+                best_t = t0;
+                best_i = i;
+                best_f = 0;
+              }
+            }
+          };
+          // scale + translation spheres take the diagonal transform (exact, see axis_o)
+          const bool rax = wave_all(!tr || (axis_o_ok(ray.o) && axis_d_ok(ray.d)));
           for (int r = 0; r < P.nruns; r++) {
             const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
-              scan_records<0>(cgeo, r0, rn, [&](int i, const Rec12& R) {
-                const Ray l = to_obj(R.m, ray);
-                const double a = dot(l.d, l.d);
-                const double hb = dot(l.o, l.d);
-                const double c = dot(l.o, l.o) - 1.0;
-                const double disc = hb * hb - a * c;
-                if (tr && !(disc < 0.0)) {
-                  const double t0 = (-hb - gsqrt(disc)) / a;
-                  if (t0 > 0.0 && (!found || t0 < best_t)) {
-                    found = true;
-                    best_t = t0;
-                    best_i = i;
-                    best_f = 0;
-                  }
-                }
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && rax) {
+              scan_records<0, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
+                Ray l;
+                l.o = axis_o(R.m, ray.o);
+                l.d = axis_d(R.m, ray.d);
+                tsphere(i, l);
               }, [] { return false; });
+            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
+              scan_records<0>(cgeo, r0, rn, [&](int i, const Rec12& R) { tsphere(i, to_obj(R.m, ray)); },
+                              [] { return false; });
             } else {
               for (int i = r0; i < r0 + rn; i++) trace_obj(i, rk, S.geo + (size_t)i * GEO, tr);
             }
@@ -2213,7 +2352,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         bd_trays++;
 #endif
         int ssp = 0;
-        bst.push(ssp, lane, 0, __ballot(tr));
+        bst.push(ssp, lane, 0, wave_ballot(tr));
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
@@ -2241,11 +2380,11 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const int* ni = reinterpret_cast<const int*>(nb + 12);
             const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
             float t0 = 0.0f, t1 = 0.0f;  // (set by may_hit_box when it returns true)
-            const bool a0 = act && may_hit_box(of, idf, slack, tmax, nb, t0);
-            const bool a1 = act && may_hit_box(of, idf, slack, tmax, nb + 6, t1);
-            const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+            const bool a0 = may_hit_box_a(act, of, idf, slack, tmax, nb, t0);
+            const bool a1 = may_hit_box_a(act, of, idf, slack, tmax, nb + 6, t1);
+            const uint64_t m0 = wave_ballot(a0), m1 = wave_ballot(a1);
             // near child popped first: the one most lanes enter first
-            const bool c1_first = 2 * __popcll(__ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
+            const bool c1_first = 2 * __popcll(wave_ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
             if (c1_first) {
               if (m0) bst.push(ssp, lane, ni[0], m0);
               if (m1) bst.push(ssp, lane, ni[1], m1);
@@ -2258,7 +2397,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       }
       cnt_unit(CNT_TRACED, tr);
       if (!QD && P.est_out && tr) atomicAdd(P.est_out + pout, 1u);
-      PH_MARK(1);
+      PH_MARK(2);
       d3 res = mk(0, 0, 0);
       if (tr) {
         if (found) {
@@ -2274,7 +2413,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       const bool resumed = RT_SHARE && state == S_RESUME;  // a waiting owner's helper delivered
       if (__builtin_expect(resumed, 0)) res = board_take(Bd, wait_slot());  // (not tracing: pf is false)
       unwind((tr && !found) || resumed, res, pf, pf_packed, pf_lw, pf_kr);
-      PH_MARK(2);
+      PH_MARK(3);
     }
 
     // ---- SHADE pass, once enough lanes hold a hit ----
@@ -2367,7 +2506,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     cnt_unit(CNT_SURFERR, surf_bad);
 
     // computeLighting + inShadow (raytracer.go:372-429)
-    PH_MARK(3);
+    PH_MARK(4);
     const double* M = (!spec_feat(SF_VM) || mat >= 0) ? S.mats + (size_t)mat * MAT : vmrec;
     d3 L = mk(0, 0, 0);
     if (hit) L = scale(mk(G[0], G[1], G[2]), M[9]);
@@ -2453,6 +2592,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(S.lights + (size_t)li * LGT, ldir_a[li], dist_a[li]);
 #endif
+    PH_MARK(5);
 #if RT_STREAM_SMEM && !RT_CULL && RT_SHADOW_JOINT && !defined(RT_SPEC_NOBJ)
 #define RT_JOINT_SWEEP 1
 #else
@@ -2479,38 +2619,46 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         bool any = false;
 #pragma unroll
         for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-          lon[li] = __any(jopen[li]);
+          lon[li] = wave_any(jopen[li]);
           any = any || lon[li];
         }
         return any;
       };
+      // one object against every light's shadow ray: lo = the shared
+      // object-space origin; ldir(li) = light li's object-space direction
+      auto jsphere = [&](int i, const d3 lo, auto&& ldir) {
+        const double c = dot(lo, lo) - 1.0;
+#pragma unroll
+        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+          if (!lon[li]) continue;
+          const d3 ld = ldir(li);
+          const double a = dot(ld, ld);
+          const double hb = dot(lo, ld);
+          const double disc = hb * hb - a * c;
+          if (jopen[li] && i != hit_i && !(disc < 0.0)) {
+            const double t0 = (-hb - gsqrt(disc)) / a;
+            if (t0 > 0.0 && t0 * rlen < dist_a[li]) {
+              jopen[li] = false;
+              jsend[li] = i + 1;
+            }
+          }
+        }
+      };
+      // scale + translation spheres take the diagonal transform (exact, see axis_o)
+      bool sax_l = !hit || axis_o_ok(sorig);
+#pragma unroll
+      for (int li = 0; li < RT_SPEC_NLIGHTS; li++) sax_l = sax_l && (!hit || axis_d_ok(ldir_a[li]));
+      const bool sax = wave_all(sax_l);
       for (int r = 0; r < P.nruns; r++) {
         if (!refresh()) break;
         const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-        if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
+        if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
+          scan_records<RT_SHADOW_CHECK, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
+            jsphere(i, axis_o(R.m, sorig), [&](int li) { return axis_d(R.m, ldir_a[li]); });
+          }, [&] { return !refresh(); });
+        } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
           scan_records<RT_SHADOW_CHECK>(cgeo, r0, rn, [&](int i, const Rec12& R) {
-            const double* m = R.m;
-            const d3 lo = mk(m[0] * sorig.x + m[1] * sorig.y + m[2] * sorig.z + m[3],
-                             m[4] * sorig.x + m[5] * sorig.y + m[6] * sorig.z + m[7],
-                             m[8] * sorig.x + m[9] * sorig.y + m[10] * sorig.z + m[11]);
-            const double c = dot(lo, lo) - 1.0;
-#pragma unroll
-            for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-              if (!lon[li]) continue;
-              const d3 dw = ldir_a[li];
-              const d3 ld = mk(m[0] * dw.x + m[1] * dw.y + m[2] * dw.z, m[4] * dw.x + m[5] * dw.y + m[6] * dw.z,
-                               m[8] * dw.x + m[9] * dw.y + m[10] * dw.z);
-              const double a = dot(ld, ld);
-              const double hb = dot(lo, ld);
-              const double disc = hb * hb - a * c;
-              if (jopen[li] && i != hit_i && !(disc < 0.0)) {
-                const double t0 = (-hb - gsqrt(disc)) / a;
-                if (t0 > 0.0 && t0 * rlen < dist_a[li]) {
-                  jopen[li] = false;
-                  jsend[li] = i + 1;
-                }
-              }
-            }
+            jsphere(i, to_obj_o(R.m, sorig), [&](int li) { return to_obj_d(R.m, ldir_a[li]); });
           }, [&] { return !refresh(); });
         } else {
           for (int i = r0; i < r0 + rn; i++) {
@@ -2533,6 +2681,105 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       }
     }
 #endif
+#ifndef RT_JOINT_CULL
+#define RT_JOINT_CULL 0  // small specialised scenes: one culled sweep for all shadow rays of a hit (register spills: off)
+#endif
+#if defined(RT_SPEC_NOBJ) && RT_CULL && RT_JOINT_CULL
+#define RT_JOINT_SMALL 1
+    // Small specialised scenes: one sweep over the objects for every light's
+    // shadow ray of this hit (inShadow per light, raytracer.go:411-429, each
+    // stopping at its own first occluder in index order). The rays share
+    // their origin sorig, so per object the cull's centre-minus-origin vector
+    // and padded radius (may_hit), a plane cull's f(0) (may_hit_plane), the
+    // object-space origin (rayToObjectSpace's MulPoint, raytracer.go:51-56,
+    // vec.go:298-304) and the Intersect's origin-only term (object_oc) are
+    // formed once, with the operations one to_obj + Intersect per light would
+    // use: verdicts and counts are bit-identical.
+    bool jopen[RT_SPEC_NLIGHTS];
+    int jsend[RT_SPEC_NLIGHTS];
+    {
+      const F3 sof = f3(sorig);
+      const float sslack = ray_slack(sof);
+      F3 jdf[RT_SPEC_NLIGHTS];
+      float jtmax[RT_SPEC_NLIGHTS];
+#pragma unroll
+      for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+        jopen[li] = hit;
+        jsend[li] = P.nobj;
+        jdf[li] = f3(ldir_a[li]);
+#if RT_STMAX_F32
+        jtmax[li] = (float)dist_a[li] * rlen_rcpf * 1.0001f + 1e-4f;
+#else
+        jtmax[li] = (float)(dist_a[li] / rlen) * 1.0001f + 1e-4f;
+#endif
+      }
+#pragma unroll
+      for (int i = 0; i < RT_SPEC_NOBJ; i++) {
+        const int k = spec_kinds[i];
+        const double* g = S.geo + (size_t)i * GEO;
+        bool tst[RT_SPEC_NLIGHTS];
+        bool anyt = false;
+        if (k != RT_PLANE) {
+          const float* b = reinterpret_cast<const float*>(g + 12);
+          const float ox = b[0] - sof.x, oy = b[1] - sof.y, oz = b[2] - sof.z;
+          const float R = b[3] + sslack;
+          const float r2 = R * R;
+#pragma unroll
+          for (int li = 0; li < RT_SPEC_NLIGHTS; li++)
+            tst[li] = may_hit_oc_a(CULL_AND(jopen[li], i != hit_i), ox, oy, oz, r2, jdf[li], jtmax[li]);
+        } else {
+          const double* sh = S.shade + (size_t)i * SHD;
+          const PlaneO po = may_hit_plane_o(sof, sh);
+#pragma unroll
+          for (int li = 0; li < RT_SPEC_NLIGHTS; li++)
+            tst[li] = CULL_AND(CULL_AND(jopen[li], i != hit_i), may_hit_plane_d(po, jdf[li], jtmax[li], sh));
+        }
+#pragma unroll
+        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) anyt = anyt || tst[li];
+        if (!wave_any(anyt)) continue;
+#ifdef RT_EXACT_DIAG
+#pragma unroll
+        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) EXDIAG(k, 1, tst[li]);
+#endif
+        if (CSG && k == RT_CSG) {
+#pragma unroll
+          for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+            if (tst[li]) {
+              Ray sr;
+              sr.o = sorig;
+              sr.d = ldir_a[li];
+              double t;
+              int f;
+              if (csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist_a[li], false) && t * rlen < dist_a[li]) {
+                jopen[li] = false;
+                jsend[li] = i + 1;
+              }
+            }
+          }
+          continue;
+        }
+        if (anyt) {
+          Ray l;
+          l.o = to_obj_o(g, sorig);
+          const double oc = object_oc(k, g, l.o);
+#pragma unroll
+          for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+            if (tst[li]) {
+              l.d = to_obj_d(g, ldir_a[li]);
+              double t;
+              int f;
+              if (object_hit_l(k, g, l, oc, t, f) && t * rlen < dist_a[li]) {
+                jopen[li] = false;
+                jsend[li] = i + 1;
+              }
+            }
+          }
+        }
+      }
+    }
+#else
+#define RT_JOINT_SMALL 0
+#endif
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
       const double* lt = S.lights + (size_t)li * LGT;
@@ -2540,6 +2787,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       const d3 ldir = ldir_a[li];
       const double dist = dist_a[li];
 #else
+#define RT_JOINT_SMALL 0
     for (int li = 0; li < P.nlights; li++) {
       const double* lt = S.lights + (size_t)li * LGT;
       const int lkind = (int)lt[9];  // wave-uniform
@@ -2567,9 +2815,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       int send = P.nobj;
       if constexpr (!BVH) {
 #ifdef RT_SPEC_NOBJ
+#if RT_JOINT_SMALL
+        open = jopen[li];  // the joint sweep above
+        send = jsend[li];
+        constexpr int SH_NOBJ = 0;
+#else
+        constexpr int SH_NOBJ = RT_SPEC_NOBJ;
+#endif
 #pragma unroll
-        for (int i = 0; i < RT_SPEC_NOBJ; i++) {
-          if (!__any(open)) break;
+        for (int i = 0; i < SH_NOBJ; i++) {
+          if (!wave_any(open)) break;
           const int k = spec_kinds[i];
 #else
         if constexpr (STREAM) {
@@ -2581,27 +2836,36 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           // first occluder (raytracer.go:411-429), the wave once no lane is open
           // (tested every RT_SHADOW_CHECK objects: a closed lane never reopens).
           const cdptr cgeo = (cdptr)S.geo;
+          auto ssphere = [&](int i, const Ray& l) {
+            const double a = dot(l.d, l.d);
+            const double hb = dot(l.o, l.d);
+            const double c = dot(l.o, l.o) - 1.0;
+            const double disc = hb * hb - a * c;
+            if (open && i != hit_i && !(disc < 0.0)) {
+              const double t0 = (-hb - gsqrt(disc)) / a;
+              if (t0 > 0.0 && t0 * rlen < dist) {
+                open = false;
+                send = i + 1;
+              }
+            }
+          };
+          const bool sax = wave_all(!hit || (axis_o_ok(sr.o) && axis_d_ok(sr.d)));
           for (int r = 0; r < P.nruns; r++) {
-            if (!__any(open)) break;
+            if (!wave_any(open)) break;
             const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
-              scan_records<RT_SHADOW_CHECK>(cgeo, r0, rn, [&](int i, const Rec12& R) {
-                const Ray l = to_obj(R.m, sr);
-                const double a = dot(l.d, l.d);
-                const double hb = dot(l.o, l.d);
-                const double c = dot(l.o, l.o) - 1.0;
-                const double disc = hb * hb - a * c;
-                if (open && i != hit_i && !(disc < 0.0)) {
-                  const double t0 = (-hb - gsqrt(disc)) / a;
-                  if (t0 > 0.0 && t0 * rlen < dist) {
-                    open = false;
-                    send = i + 1;
-                  }
-                }
-              }, [&] { return !__any(open); });
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
+              scan_records<RT_SHADOW_CHECK, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
+                Ray l;
+                l.o = axis_o(R.m, sr.o);
+                l.d = axis_d(R.m, sr.d);
+                ssphere(i, l);
+              }, [&] { return !wave_any(open); });
+            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE) {
+              scan_records<RT_SHADOW_CHECK>(cgeo, r0, rn, [&](int i, const Rec12& R) { ssphere(i, to_obj(R.m, sr)); },
+                                            [&] { return !wave_any(open); });
             } else {
               for (int i = r0; i < r0 + rn; i++) {
-                if (!__any(open)) break;
+                if (!wave_any(open)) break;
                 if (open && i != hit_i) {
                   double t;
                   int f;
@@ -2615,12 +2879,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           }
 #else
           stream_objects([&](int i, int k, const double* g) {
-            if (!__any(open)) return false;
-            bool test = open && i != hit_i;
+            if (!wave_any(open)) return false;
+            bool test = CULL_AND(open, i != hit_i);
 #if RT_CULL
-            test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
-                                          : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
-            if (!__any(test)) return true;
+            test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
+                                 : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+            if (!wave_any(test)) return true;
 #endif
             EXDIAG(k, 1, test);
             if (test) {
@@ -2636,19 +2900,19 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #endif
         }
         for (int i = STREAM ? P.nobj : 0; i < P.nobj; i++) {
-          if (!__any(open)) break;
+          if (!wave_any(open)) break;
           const int k = S.kind[i];
 #endif
           const double* g = S.geo + (size_t)i * GEO;
-          bool test = open && i != hit_i;
+          bool test = CULL_AND(open, i != hit_i);
 #if RT_SHADOW_HOISTED
-          test = test && (k != RT_PLANE ? may_hit_oc(cox[i], coy[i], coz[i], cr2[i], sdf, stmax)
-                                        : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
-          if (!__any(test)) continue;
+          test = k != RT_PLANE ? may_hit_oc_a(test, cox[i], coy[i], coz[i], cr2[i], sdf, stmax)
+                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!wave_any(test)) continue;
 #elif RT_CULL
-          test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
-                                        : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
-          if (!__any(test)) continue;
+          test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
+                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!wave_any(test)) continue;
 #endif
           EXDIAG(k, 1, test);
           if (test) {
@@ -2676,10 +2940,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         // counts per kind. The shadow verdict is the same either way.
         int occ = 0x7fffffff;
         auto shadow_obj = [&](int i, int k, const double* g, bool act) {
-          bool test = act && i != hit_i && i < occ;
-          test = test && (k != RT_PLANE ? may_hit(sof, sdf, stmax, g, sslack)
-                                        : may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
-          if (!__any(test)) return;
+          bool test = CULL_AND(CULL_AND(act, i != hit_i), i < occ);
+          test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
+                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!wave_any(test)) return;
           EXDIAG(k, 1, test);
           if (test) {
             double t;
@@ -2704,7 +2968,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         bd_srays++;
 #endif
         int ssp = 0;
-        bst.push(ssp, lane, 0, __ballot(hit));
+        bst.push(ssp, lane, 0, wave_ballot(hit));
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
@@ -2731,15 +2995,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
             const int* ni = reinterpret_cast<const int*>(nb + 12);
             float t0 = 0.0f, t1 = 0.0f;
-            const bool a0 = act && ni[2] < occ && may_hit_box(sof, sidf, sslack, stmax, nb, t0);
-            const bool a1 = act && ni[3] < occ && may_hit_box(sof, sidf, sslack, stmax, nb + 6, t1);
-            const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+            const bool a0 = may_hit_box_a(CULL_AND(act, ni[2] < occ), sof, sidf, sslack, stmax, nb, t0);
+            const bool a1 = may_hit_box_a(CULL_AND(act, ni[3] < occ), sof, sidf, sslack, stmax, nb + 6, t1);
+            const uint64_t m0 = wave_ballot(a0), m1 = wave_ballot(a1);
 #ifndef RT_SHADOW_NEAR_FIRST
 #define RT_SHADOW_NEAR_FIRST 0  // measured: near-first shadow order is slower (C5 695 -> 822 ms)
 #endif
 #if RT_SHADOW_NEAR_FIRST
             // nearer subtree popped first: finds an occluder soonest
-            const bool c1_first = 2 * __popcll(__ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
+            const bool c1_first = 2 * __popcll(wave_ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
 #else
             // lower-index subtree popped first: it can prune the other
             const bool c1_first = ni[3] < ni[2];
@@ -2767,7 +3031,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if (spec_kind(4) && (P.kind_mask & 16)) cnt_kind(4, pe4 - (hk == 4 ? 1u : 0u));  // cones, CSG: rare, flushed per light
         if (spec_kind(5) && (P.kind_mask & 32)) cnt_kind(5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
       }
-      PH_MARK(4);
+      PH_MARK(6);
 #if defined(RT_SPEC_NLIGHTS) && RT_LIGHT_SPLIT
       open_a[li] = hit && open;
       (void)lkind;
@@ -2800,7 +3064,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         L = add(add(L, diffuse), specular);
       }
     }
-    PH_MARK(5);
+    PH_MARK(7);
 #else
       if (hit && open) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
@@ -2815,7 +3079,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         d3 specular = scale(lcol, M[10] * go_pow(spec, M[11], (int)G[11]));
         L = add(add(L, diffuse), specular);
       }
-      PH_MARK(5);
+      PH_MARK(7);
     }
 #endif
     if (hit) {
@@ -2908,9 +3172,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         }
       }
     }
-    PH_MARK(6);
+    PH_MARK(8);
     unwind(have_res, res, false, 0, mk(0, 0, 0), 0.0);
-    PH_MARK(7);
+    PH_MARK(9);
   }
   if (RT_PIX_BATCH) flush_pixels();
 

@@ -51,12 +51,14 @@ def deinterleave(slabs, height):
 _recv = {}
 
 
-def gather_frame(buf, height, mode="bands", group=None, collective=None):
+def gather_frame(buf, height, mode="bands", group=None, collective=None, slot=None):
     """Gather every rank's buffer to rank 0 and assemble the [H, W, 4] frame
     there (None elsewhere). Rank 0 receives straight into the slices of one
-    reused [world, ...] tensor (no stacking copy). With a single rank the
-    buffer already is the frame and no collective runs, unless `collective`
-    is True (tests: the RCCL gather at world size 1)."""
+    reused [world, ...] tensor per `slot` (no stacking copy; frames in flight
+    on different streams use different slots, so one frame's receive tensor is
+    never overwritten while another stream still reads it). With a single rank
+    the buffer already is the frame and no collective runs, unless
+    `collective` is True (tests: the RCCL gather at world size 1)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -66,7 +68,7 @@ def gather_frame(buf, height, mode="bands", group=None, collective=None):
         return deinterleave(buf.unsqueeze(0), height) if mode == "interleaved" else buf[:height]
     rank = dist.get_rank(group)
     if rank == 0:
-        key = (tuple(buf.shape), buf.dtype, buf.device, world)
+        key = (tuple(buf.shape), buf.dtype, buf.device, world, "sync", slot)
         stacked = _recv.get(key)
         if stacked is None:
             stacked = _recv[key] = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
@@ -243,7 +245,12 @@ class DistributedRenderer:
                     # issued on the launch stream: the collective waits for this render only
                     self.pending[slot] = gather_frame_async(buf, self.H, self.mode, slot)
                     return None  # the frame comes from flush() / a later step
-                self.frame = gather_frame(buf, self.H, self.mode, collective=collective)
+                self.frame = gather_frame(buf, self.H, self.mode, collective=collective,
+                                          slot=slot if self.inflight > 1 else None)
+        if gather and stream is not None:
+            # the frame was gathered and assembled on the launch stream: the
+            # caller's stream (which reads it) is ordered after it
+            torch.cuda.current_stream().wait_stream(stream)
         return self.frame
 
     def flush(self):

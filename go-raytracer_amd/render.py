@@ -134,10 +134,13 @@ class RenderContext:
         return self.packed
 
     def set_specialize(self, enable=True):
-        """Render small linear scenes (<= 8 objects) with a kernel compiled for
-        their object kinds (hipRTC, ~1-2 s once per scene shape and process;
-        bit-identical output). Raises RenderError if hipRTC fails."""
-        _check(self.lib.rt_set_specialize(self.handle, int(bool(enable))), "rt_set_specialize")
+        """Render with a kernel compiled for the scene's shape (hipRTC, ~1-2 s
+        once per scene shape and process; bit-identical output). Raises
+        RenderError if hipRTC fails. enable="async": compile in the background
+        and run the generic kernel until it is done (abi.RT_SPECIALIZE_ASYNC)."""
+        from . import abi
+        mode = abi.RT_SPECIALIZE_ASYNC if enable == "async" else int(bool(enable))
+        _check(self.lib.rt_set_specialize(self.handle, mode), "rt_set_specialize")
 
     def set_accel(self, flags):
         """abi.RT_ACCEL_BVH | abi.RT_ACCEL_CULL (default both). 0 = the
@@ -275,13 +278,16 @@ class RenderContext:
 
 
 def kernel_source_id():
-    """Identifier of the device code (sha256 of the kernel sources, 16 hex
-    digits): stored with committed PMC summaries so that a bench line only
-    quotes counters recorded with the kernel it times."""
+    """Identifier of the device code and its launch configuration (sha256 of
+    the kernel sources and of rt_kernel.hip -- occupancy bounds, hipRTC flags,
+    schedule choice, tile order, grid sizing -- 16 hex digits): stored with
+    committed PMC summaries so that a bench line only quotes counters recorded
+    with the kernel and launches it times."""
     import hashlib
     h = hashlib.sha256()
     root = os.path.dirname(PKG_DIR)
-    for rel in ("include/rt_abi.h", "go-raytracer_amd/csrc/rt_device.h", "go-raytracer_amd/csrc/rt_render.h"):
+    for rel in ("include/rt_abi.h", "go-raytracer_amd/csrc/rt_device.h", "go-raytracer_amd/csrc/rt_render.h",
+                "go-raytracer_amd/csrc/rt_kernel.hip"):
         with open(os.path.join(root, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]

@@ -209,7 +209,7 @@ static inline double go_exp_amd64(double x, int fma_) {
     y = y + T[1];
     /* return y * 2**e: biased exponent e + 1023 as bits */
     int32_t b = e + 0x3FF;
-    if (b < 0) { /* denormal */
+    if (b <= 0) { /* denormal (exp_amd64.s: JLE after the bias add) */
         if (b < -52) return 0.0;
         b += 0x3FE;
         y = y * go_bits_f64((uint64_t)(uint32_t)b << 52);

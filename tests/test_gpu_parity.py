@@ -548,6 +548,54 @@ def test_specialised_full_4k_c3_equals_generic(ctx, spec_ctx):
     assert spec_ctx.specialized() == (True, 0.0)  # cached: no second compile
 
 
+def test_async_specialisation_equals_oracle():
+    """rt_set_specialize(RT_SPECIALIZE_ASYNC): the generic kernel until the
+    background compile is done, then the specialised one; every frame equals
+    the oracle (bytes + counters) whichever kernel rendered it."""
+    import time
+    packed = rt.scene.convert(rt.configs.c3(width=96, height=64))
+    ref, ost = oracle_bind.render_rows(packed)
+    c = rt.RenderContext(0, specialize="async")
+    try:
+        kernels = []
+        t_end = time.time() + 120
+        while True:
+            img, st = render(c, packed)  # (set_scene every time, as rt_render does)
+            assert_same(img, ref, "async specialisation")
+            assert st.as_dict() == ost.as_dict()
+            kernels.append(bool(c.specialized()[0]))
+            if kernels[-1] or time.time() > t_end:
+                break
+            time.sleep(0.1)
+        assert kernels[-1], "the background compile never finished"
+        img, st = render(c, packed)
+        assert_same(img, ref, "async specialisation (compiled)")
+    finally:
+        c.close()
+
+
+def test_rt_render_repeated_calls_equal_oracle():
+    """rt_render (the synchronous Render() seam, raytracer.go:589) called
+    repeatedly from one process on alternating scenes: cached context and
+    frame buffer, background specialisation -- every image and counter set
+    equal to the oracle's."""
+    import ctypes
+    lib = rt.render.load_library()
+    scenes = [rt.scene.convert(rt.configs.c3(width=80, height=48)),
+              rt.scene.convert(rt.configs.canned(width=95, height=60)),
+              rt.scene.convert(rt.configs.c2(width=64, height=36))]
+    refs = [oracle_bind.render_rows(p) for p in scenes]
+    for k in range(9):
+        p = scenes[k % 3]
+        ref, ost = refs[k % 3]
+        out = np.empty((p.height, p.width, 4), np.uint8)
+        st = rt.abi.rt_stats()
+        assert lib.rt_render(p.ref(), out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)) == 0, \
+            lib.rt_last_error()
+        assert_same(out, ref, "rt_render call %d" % k)
+        assert st.as_dict() == ost.as_dict()
+
+
 # --- rt_set_accel: the reference's brute-force search (no BVH, no culling)
 # must give the same pixels and counters as the accelerated search.
 
@@ -615,6 +663,58 @@ def test_streamed_brute_force_c5_band_matches_oracle(ctx, spec_ctx):
         assert_same(img, ref, "brute-force c5 band")
         assert st.as_dict() == ost.as_dict()
         assert st.tests[rt.abi.RT_SPHERE] == 100000 * (st.primary_rays + st.secondary_rays)
+
+
+def _axis_scene(seed, n, width, height, depth=6):
+    """Spheres whose WorldToObject is a scale + translation (the diagonal
+    transform of the brute-force sphere runs, rt_render.h axis_o) in runs
+    interleaved with rotated spheres, spheres with a zero translation
+    component (full form: the diagonal form needs m3, m7, m11 != 0),
+    non-uniform scales, exact-tie duplicates, reflective and glass materials,
+    a plane and a cube between the runs."""
+    import random
+    rng = random.Random(seed)
+    mats = [S.material((rng.random(), rng.random(), rng.random()), rng.choice([0.0, 0.3, 0.6]), 0.0,
+                       rng.choice([0.0, 0.0, 0.8]), 1.3 + 0.4 * rng.random(), 0.9, 0.5, float(rng.choice([5, 20])))
+            for _ in range(5)]
+    objs = []
+    for i in range(n):
+        m = rng.choice(mats)
+        x, y, z = rng.uniform(-3, 3), rng.uniform(-1.5, 1.5), rng.uniform(3, 9)
+        r = 0.1 + 0.25 * rng.random()
+        mode = (i // 9) % 4  # runs of 9 of one form
+        if mode == 0:
+            o = S.Sphere(m).uscale(r).translate(x, y, z)
+        elif mode == 1:
+            o = S.Sphere(m).scale(r, 1.5 * r, 0.7 * r).translate(x, y, z)
+        elif mode == 2:
+            o = S.Sphere(m).uscale(r).rotatey(rng.uniform(-60, 60)).translate(x, y, z)
+        else:
+            o = S.Sphere(m).uscale(r).translate(0.0 if i % 2 else x, y, 0.0 if i % 3 == 0 else z)
+        objs.append(o)
+        if i % 11 == 5:
+            objs.append(replace(o, surface=rng.choice(mats)))  # exact t ties: the first index wins
+        if i == n // 2:
+            objs.append(S.Cube(mats[0]).uscale(0.5).translate(0.5, -1.0, 6.0))
+    objs.append(S.Plane(mats[1]).translate(0.0, -2.0, 0.0))
+    lights = [S.PointLight((5.0, 6.0, 0.0), (0.6, 0.6, 0.6)), S.PointLight((-4.0, 3.0, 2.0), (0.4, 0.5, 0.4))]
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=S.Union(tuple(objs)), depth=depth,
+                        fov=75.0, width=width, height=height, bg_start=(0.0, 0.0, 0.0), bg_end=(0.5, 0.7, 1.0))
+
+
+@pytest.mark.parametrize("seed,n", [(7, 180), (8, 300)])
+def test_brute_force_axis_sphere_runs_match_oracle(ctx, spec_ctx, seed, n):
+    """Brute-force search over scale + translation sphere runs (diagonal
+    rayToObjectSpace, exact by the argument at rt_render.h axis_o) mixed with
+    full-form runs: the specialised kernel's scalar-load sweeps (trace, joint
+    shadow sweep) and the generic kernel's stream, bytes + counters."""
+    packed = rt.scene.convert(_axis_scene(seed, n, 96, 64))
+    ref, ost = oracle_bind.render_rows(packed)
+    for c in (ctx, spec_ctx):
+        img, st, info = _brute(c, packed)
+        assert not info & (rt.abi.RT_INFO_LDS | rt.abi.RT_INFO_BVH), info
+        assert_same(img, ref, "axis runs seed %d n %d" % (seed, n))
+        assert st.as_dict() == ost.as_dict()
 
 
 # --- math.Pow with fractional exponents (Go exp.go / log.go restated on both

@@ -157,6 +157,10 @@ def test_go_exp_amd64_restatement():
         assert e(0.0) == 1.0 and e(float("-inf")) == 0.0 and e(float("inf")) == float("inf")
         assert math.isnan(e(float("nan"))) and e(709.79) == float("inf") and e(-1e10) == 0.0
         assert e(-745.0) == 5e-324 and e(-740.0) == 4.2e-322  # the two-factor denormal path
+        # biased exponent exactly 0 (e = -1023) takes the denormal path too
+        # (exp_amd64.s branches with JLE): a subnormal within 4 ulp, not 0
+        for x in (-709.5, -709.2, -709.7):
+            assert 0.0 < e(x) < 2.2250738585072014e-308 and _ulps(e(x), math.exp(x)) <= 4, x
         rng = np.random.default_rng(7 + f)
         for x in rng.uniform(-700, 700, 20000):
             assert _ulps(e(x), math.exp(x)) <= 4, x
