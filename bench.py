@@ -239,11 +239,12 @@ def render_api_leg(pkg, packed, reps=30, budget_s=20.0):
     (raytracer.go:589-682, hooked at evaluator.go:48): every call converts and
     uploads the scene (rt_set_scene), renders one frame on the library's cached
     context and copies the RGBA8 image into pageable host memory (numpy), like
-    Go's image.RGBA. Its context specialises in the background
-    (RT_SPECIALIZE_ASYNC): the first calls with a new scene shape run the
-    generic kernel. Reported: the first call in the process (context creation
-    included), the median of the last five of `reps` calls, and one warm call
-    split into its parts through a RenderContext (scene setup, kernel, D2H)."""
+    Go's image.RGBA. Its context specialises the kernel (rt_set_specialize; the
+    first call with a new scene shape pays the hipRTC compile unless this
+    process already compiled that shape). Reported: the first call in the
+    process (context creation included), the median of the last five of `reps`
+    calls, and one warm call split into its parts through a RenderContext
+    (scene setup, kernel, D2H)."""
     import ctypes
     import numpy as np
     import torch
@@ -261,8 +262,8 @@ def render_api_leg(pkg, packed, reps=30, budget_s=20.0):
         if k >= 5 and time.perf_counter() > t_end:
             break
     last = sorted(times[-5:])
-    # one warm call's parts, on a RenderContext with the same (async) specialisation
-    ctx = pkg.RenderContext(torch.cuda.current_device(), specialize="async")
+    # one warm call's parts, on a RenderContext with the same specialisation
+    ctx = pkg.RenderContext(torch.cuda.current_device(), specialize=True)
     try:
         for _ in range(3):
             t0 = time.perf_counter()

@@ -5,8 +5,7 @@ sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
-RT_ABI_VERSION = 5  # include/rt_abi.h
-RT_SPECIALIZE_ASYNC = 2  # rt_set_specialize: background compile
+RT_ABI_VERSION = 4  # include/rt_abi.h
 RT_EXP_AMD64_FMA, RT_EXP_AMD64, RT_EXP_PORTABLE = 0, 1, 2  # rt_scene.exp_mode
 
 RT_OK = 0

@@ -39,8 +39,6 @@
 #include <chrono>
 #include <functional>
 #include <cmath>
-#include <set>
-#include <thread>
 #include <array>
 #include <cstdio>
 #include <utility>
@@ -532,8 +530,6 @@ struct rt_context {
   // scene specialisation (rt_set_specialize)
   bool specialize = false;
   int accel = RT_ACCEL_BVH | RT_ACCEL_CULL;  // rt_set_accel
-  bool spec_async = false;          // rt_set_specialize(RT_SPECIALIZE_ASYNC): compile in the background
-  bool spec_waiting = false;        // ... and the current scene's kernel is still compiling
   hipFunction_t spec_fn = nullptr;  // specialised kernel of the current scene, if any
   hipFunction_t spec_alt_fn[3] = {nullptr, nullptr, nullptr};  // ... for the other pixel schedules (spec_for)
   SpecKey spec_key;                     // what spec_fn was compiled for
@@ -616,23 +612,6 @@ std::mutex g_spec_mu;
 Rtc g_rtc;
 std::map<std::string, SpecCode> g_spec_code;
 std::map<std::pair<int, std::string>, hipFunction_t> g_spec_fn;
-// Background compiles (RT_SPECIALIZE_ASYNC): keys in progress or failed, and
-// the threads, joined at exit (declared after the caches above, so destroyed
-// before them).
-std::mutex g_bg_mu;
-std::set<std::string> g_spec_busy, g_spec_failed;
-std::vector<std::thread> g_bg_threads;
-struct BgJoin {
-  ~BgJoin() {
-    std::vector<std::thread> t;
-    {
-      std::lock_guard<std::mutex> l(g_bg_mu);
-      t.swap(g_bg_threads);
-    }
-    for (auto& x : t)
-      if (x.joinable()) x.join();
-  }
-} g_bg_join;
 
 // Caller holds g_spec_mu.
 bool rtc_load() {
@@ -925,48 +904,10 @@ int spec_build(int device, const SpecKey& sk, hipFunction_t* fn, double* ms) {
   return RT_OK;
 }
 
-// Start compiling `sk` on a background thread (no-op if it is compiling,
-// compiled or failed before).
-void spec_compile_bg(const SpecKey& sk) {
-  const std::string key = sk.str();
-  std::lock_guard<std::mutex> l(g_bg_mu);
-  if (g_spec_busy.count(key) || g_spec_failed.count(key)) return;
-  g_spec_busy.insert(key);
-  g_bg_threads.emplace_back([sk, key] {
-    double ms = 0;
-    int rc;
-    {
-      std::lock_guard<std::mutex> lock(g_spec_mu);
-      rc = spec_compile(sk, &ms);
-    }
-    std::lock_guard<std::mutex> l2(g_bg_mu);
-    g_spec_busy.erase(key);
-    if (rc != RT_OK) g_spec_failed.insert(key);
-  });
-}
-
-// RT_SPECIALIZE_ASYNC: point c->spec_fn at the current scene's specialised
-// kernel once its background compile is done (never blocks on a compile).
-void spec_poll(rt_context* c) {
-  std::unique_lock<std::mutex> lock(g_spec_mu, std::try_to_lock);
-  if (!lock.owns_lock()) return;  // a compile is running
-  const std::string key = c->spec_key.str();
-  if (g_spec_code.count(key)) {
-    c->spec_waiting = false;
-    double ms = 0;
-    if (spec_build(c->device, c->spec_key, &c->spec_fn, &ms) != RT_OK) c->spec_fn = nullptr;
-    return;
-  }
-  lock.unlock();
-  std::lock_guard<std::mutex> l(g_bg_mu);
-  if (g_spec_failed.count(key)) c->spec_waiting = false;  // stays generic
-}
-
 // Point c->spec_fn at the specialised kernel of the current scene (or clear it).
 int spec_prepare(rt_context* c) {
   c->spec_fn = nullptr;
   c->spec_ms = 0;
-  c->spec_waiting = false;
   if (!c->specialize || !c->has_scene) return RT_OK;
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
@@ -976,13 +917,6 @@ int spec_prepare(rt_context* c) {
   if (sk.share && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the board assumes one owner lane per pixel
   c->spec_key = sk;
   for (auto& f : c->spec_alt_fn) f = nullptr;
-  if (c->spec_async) {
-    // the generic kernel until the background compile is done (spec_poll)
-    c->spec_waiting = true;
-    spec_poll(c);
-    if (c->spec_waiting) spec_compile_bg(sk);
-    return RT_OK;
-  }
   std::lock_guard<std::mutex> lock(g_spec_mu);
   return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
 }
@@ -993,22 +927,6 @@ int spec_for(rt_context* c, int sch, hipFunction_t* fn) {
   if (c->spec_fn && c->spec_key.share && sch == SCH_PAIRS) sch = SCH_QUADS;
   if (!c->spec_fn || c->spec_key.quads == sch) {
     *fn = c->spec_fn;
-    return RT_OK;
-  }
-  if (c->spec_async) {  // another schedule: generic until its compile is done
-    SpecKey sk = c->spec_key;
-    sk.quads = sch;
-    std::unique_lock<std::mutex> lock(g_spec_mu, std::try_to_lock);
-    if (lock.owns_lock() && g_spec_code.count(sk.str())) {
-      double ms = 0;
-      int rc = spec_build(c->device, sk, &c->spec_alt_fn[sch], &ms);
-      if (rc != RT_OK) return rc;
-      *fn = c->spec_alt_fn[sch];
-      return RT_OK;
-    }
-    if (lock.owns_lock()) lock.unlock();
-    spec_compile_bg(sk);
-    *fn = nullptr;
     return RT_OK;
   }
   if (!c->spec_alt_fn[sch]) {
@@ -1053,9 +971,7 @@ int rt_set_frames_in_flight(rt_context* c, int n) {
 
 int rt_set_specialize(rt_context* c, int enable) {
   if (!c) return fail(RT_E_INVALID, "rt_set_specialize: NULL context");
-  if (enable < 0 || enable > RT_SPECIALIZE_ASYNC) return fail(RT_E_INVALID, "rt_set_specialize: unknown mode");
   c->specialize = enable != 0;
-  c->spec_async = enable == RT_SPECIALIZE_ASYNC;
   return spec_prepare(c);
 }
 
@@ -1747,7 +1663,6 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
   // loads instead: no stream buffers)
   // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)
-  if (c->spec_waiting && !est) spec_poll(c);  // RT_SPECIALIZE_ASYNC: its compile may be done now
   static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
@@ -2186,10 +2101,13 @@ int rt_render(const rt_scene* scene, uint8_t* rgba_out, rt_stats* stats) {
   if (!sl.c) {
     int rc = rt_create(dev, &sl.c);
     if (rc != RT_OK) return rc;
+    // scene specialisation (hipRTC, cached per process by scene shape): the
+    // first call with a new shape pays the compile; RT_RENDER_SPECIALIZE=0 keeps
+    // the generic kernel (hipRTC runs in its own link-map namespace with its own
+    // libc, so it is only ever called on the caller's thread)
     const char* e = getenv("RT_RENDER_SPECIALIZE");
-    const int mode = e ? atoi(e) : RT_SPECIALIZE_ASYNC;
-    if (mode) {
-      rc = rt_set_specialize(sl.c, mode == 1 ? 1 : RT_SPECIALIZE_ASYNC);
+    if (!e || atoi(e) != 0) {
+      rc = rt_set_specialize(sl.c, 1);
       if (rc != RT_OK) return rc;
     }
   }

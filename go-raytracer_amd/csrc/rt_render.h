@@ -312,6 +312,8 @@ __device__ __forceinline__ d3 axis_d(const double* a, d3 d) { return mk(a[0] * d
 // WorldToObject doubles), which land in SGPRs and feed the FP64 VALU ops as
 // their scalar operand -- no LDS or vector-memory bandwidth per object.
 typedef const __attribute__((address_space(4))) double* cdptr;
+typedef const __attribute__((address_space(4))) float* cfptr;
+typedef const __attribute__((address_space(4))) int* ciptr;
 template <int N>
 struct RecN {
   double m[N];
@@ -325,6 +327,28 @@ __device__ __forceinline__ RecN<N> ld_rec(cdptr p) {
 #pragma unroll
   for (int q = 0; q < N; q++) r.m[q] = p[q];
   return r;
+}
+// A BVH leaf object's record (bvh_geo: GEO doubles in leaf order; 0..11
+// WorldToObject, 12..13 the FP32 bounding sphere, 14 index, 15 kind) read
+// through the constant address space: the index is wave-uniform, so this is
+// two scalar loads into SGPRs instead of vector loads per lane.
+struct LeafRec {
+  RecN<12> R;
+  float cx, cy, cz, cr;
+  int i, k;
+};
+__device__ __forceinline__ LeafRec ld_leaf(const double* base, int j) {
+  const cdptr p = (cdptr)base + (size_t)j * 16;
+  LeafRec L;
+  L.R = ld_rec<12>(p);
+  const uint64_t b0 = (uint64_t)__double_as_longlong(p[12]), b1 = (uint64_t)__double_as_longlong(p[13]);
+  L.cx = __int_as_float((int)(uint32_t)b0);
+  L.cy = __int_as_float((int)(uint32_t)(b0 >> 32));
+  L.cz = __int_as_float((int)(uint32_t)b1);
+  L.cr = __int_as_float((int)(uint32_t)(b1 >> 32));
+  L.i = (int)(uint32_t)(uint64_t)__double_as_longlong(p[14]);
+  L.k = (int)(uint32_t)(uint64_t)__double_as_longlong(p[15]);
+  return L;
 }
 // Index of the next record to prefetch, made to depend on the current record
 // (an empty asm that "reads" it): scalar loads return out of order, so the
@@ -719,14 +743,19 @@ __device__ __forceinline__ bool may_hit_oc(float ox, float oy, float oz, float r
 // inactive lane compares against an unreachable bound), so the result is one
 // compare's lane mask: the wave's any-lane test reads it directly (a && of
 // two lane masks is rematerialised through a VGPR before a ballot).
-__device__ __forceinline__ bool may_hit_a(bool act, F3 o, F3 d, float tmax, const double* g, float slack) {
-  const float* b = reinterpret_cast<const float*>(g + 12);
-  float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
+// (c: the bounding sphere's centre and padded radius, b[0..3] of may_hit)
+__device__ __forceinline__ bool may_hit_s(bool act, F3 o, F3 d, float tmax, float cx, float cy, float cz, float cr,
+                                          float slack) {
+  float ox = cx - o.x, oy = cy - o.y, oz = cz - o.z;
   float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
   tc = fminf(fmaxf(tc, 0.0f), tmax);
   float qx = __builtin_fmaf(-tc, d.x, ox), qy = __builtin_fmaf(-tc, d.y, oy), qz = __builtin_fmaf(-tc, d.z, oz);
-  const float R = b[3] + slack;
+  const float R = cr + slack;
   return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= (act ? R * R : -1.0f);
+}
+__device__ __forceinline__ bool may_hit_a(bool act, F3 o, F3 d, float tmax, const double* g, float slack) {
+  const float* b = reinterpret_cast<const float*>(g + 12);
+  return may_hit_s(act, o, d, tmax, b[0], b[1], b[2], b[3], slack);
 }
 __device__ __forceinline__ bool may_hit_oc_a(bool act, float ox, float oy, float oz, float r2, F3 d, float tmax) {
   float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
@@ -754,8 +783,8 @@ __device__ __forceinline__ bool may_hit_box(F3 o, F3 id, float slack, float tmax
 // tn <= tf && tf >= 0 && tn <= tmax  <=>  max(tn, 0) <= min(tf, tmax); an
 // inactive lane's bound is -1 (a NaN tn or tmax can only admit more nodes:
 // still conservative).
-__device__ __forceinline__ bool may_hit_box_a(bool act, F3 o, F3 id, float slack, float tmax, const float* nb,
-                                              float& tn) {
+template <typename FP>
+__device__ __forceinline__ bool may_hit_box_a(bool act, F3 o, F3 id, float slack, float tmax, FP nb, float& tn) {
   const float x0 = (nb[0] - slack - o.x) * id.x, x1 = (nb[3] + slack - o.x) * id.x;
   const float y0 = (nb[1] - slack - o.y) * id.y, y1 = (nb[4] + slack - o.y) * id.y;
   const float z0 = (nb[2] - slack - o.z) * id.z, z1 = (nb[5] + slack - o.z) * id.z;
@@ -2254,15 +2283,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       // The linear loop visits objects in index order (strict <, the first
       // index wins ties); the BVH visits them in any order and breaks ties on
       // the index explicitly, which selects the same object.
-      auto trace_obj = [&](int i, int k, const double* g, bool act) {
-        bool test = act;
-#if RT_CULL
-        // an object entered beyond the lane's current best cannot win (strict <)
-        const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
-        test = k != RT_PLANE ? may_hit_a(test, of, df, tmax, g, slack)
-                             : CULL_AND(test, may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
-        if (!wave_any(test)) return;
-#endif
+      auto trace_exact = [&](int i, int k, const double* g, bool test) {
         EXDIAG(k, 0, test);
         if (test) {
           double t;
@@ -2283,6 +2304,17 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             }
           }
         }
+      };
+      auto trace_obj = [&](int i, int k, const double* g, bool act) {
+        bool test = act;
+#if RT_CULL
+        // an object entered beyond the lane's current best cannot win (strict <)
+        const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+        test = k != RT_PLANE ? may_hit_a(test, of, df, tmax, g, slack)
+                             : CULL_AND(test, may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
+        if (!wave_any(test)) return;
+#endif
+        trace_exact(i, k, g, test);
       };
       if constexpr (!BVH) {
 #ifdef RT_SPEC_NOBJ
@@ -2371,13 +2403,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #endif
             const int first = r >> 3, count = r & 7;
             for (int j = first; j < first + count; j++) {
-              const double* g = P.bvh_geo + (size_t)j * GEO;
-              const int* gi = reinterpret_cast<const int*>(g + 14);
-              trace_obj(gi[0], gi[2], g, act);
+              // the leaf's record through scalar loads (wave-uniform index)
+              const LeafRec L = ld_leaf(P.bvh_geo, j);
+              const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+              const bool test = may_hit_s(act, of, df, tmax, L.cx, L.cy, L.cz, L.cr, slack);
+              if (!wave_any(test)) continue;
+              trace_exact(L.i, L.k, L.R.m, test);
             }
           } else {
-            const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
-            const int* ni = reinterpret_cast<const int*>(nb + 12);
+            const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN;  // scalar loads
+            const ciptr ni = (ciptr)(nb + 12);
             const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
             float t0 = 0.0f, t1 = 0.0f;  // (set by may_hit_box when it returns true)
             const bool a0 = may_hit_box_a(act, of, idf, slack, tmax, nb, t0);
@@ -2939,11 +2974,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         // lower than the best so far) and derives the count from prefix
         // counts per kind. The shadow verdict is the same either way.
         int occ = 0x7fffffff;
-        auto shadow_obj = [&](int i, int k, const double* g, bool act) {
-          bool test = CULL_AND(CULL_AND(act, i != hit_i), i < occ);
-          test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
-                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
-          if (!wave_any(test)) return;
+        auto shadow_exact = [&](int i, int k, const double* g, bool test) {
           EXDIAG(k, 1, test);
           if (test) {
             double t;
@@ -2958,6 +2989,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               if (t * rlen < dist) occ = i;
             }
           }
+        };
+        auto shadow_obj = [&](int i, int k, const double* g, bool act) {
+          bool test = CULL_AND(CULL_AND(act, i != hit_i), i < occ);
+          test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
+                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+          if (!wave_any(test)) return;
+          shadow_exact(i, k, g, test);
         };
         for (int p = 0; p < P.nplanes; p++) {
           const int i = P.planes[p];
@@ -2987,13 +3025,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #endif
             const int first = r >> 3, count = r & 7;
             for (int j = first; j < first + count; j++) {
-              const double* g = P.bvh_geo + (size_t)j * GEO;
-              const int* gi = reinterpret_cast<const int*>(g + 14);
-              shadow_obj(gi[0], gi[2], g, act);
+              const LeafRec L = ld_leaf(P.bvh_geo, j);  // scalar loads
+              const bool test = may_hit_s(CULL_AND(CULL_AND(act, L.i != hit_i), L.i < occ), sof, sdf, stmax, L.cx,
+                                          L.cy, L.cz, L.cr, sslack);
+              if (!wave_any(test)) continue;
+              shadow_exact(L.i, L.k, L.R.m, test);
             }
           } else {
-            const float* nb = P.bvh_nodes + (size_t)(r >> 3) * BN;
-            const int* ni = reinterpret_cast<const int*>(nb + 12);
+            const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN;  // scalar loads
+            const ciptr ni = (ciptr)(nb + 12);
             float t0 = 0.0f, t1 = 0.0f;
             const bool a0 = may_hit_box_a(CULL_AND(act, ni[2] < occ), sof, sidf, sslack, stmax, nb, t0);
             const bool a1 = may_hit_box_a(CULL_AND(act, ni[3] < occ), sof, sidf, sslack, stmax, nb + 6, t1);

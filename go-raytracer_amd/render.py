@@ -136,11 +136,8 @@ class RenderContext:
     def set_specialize(self, enable=True):
         """Render with a kernel compiled for the scene's shape (hipRTC, ~1-2 s
         once per scene shape and process; bit-identical output). Raises
-        RenderError if hipRTC fails. enable="async": compile in the background
-        and run the generic kernel until it is done (abi.RT_SPECIALIZE_ASYNC)."""
-        from . import abi
-        mode = abi.RT_SPECIALIZE_ASYNC if enable == "async" else int(bool(enable))
-        _check(self.lib.rt_set_specialize(self.handle, mode), "rt_set_specialize")
+        RenderError if hipRTC fails."""
+        _check(self.lib.rt_set_specialize(self.handle, int(bool(enable))), "rt_set_specialize")
 
     def set_accel(self, flags):
         """abi.RT_ACCEL_BVH | abi.RT_ACCEL_CULL (default both). 0 = the

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 4
 #define RT_EXP_AMD64_FMA 0
 #define RT_EXP_AMD64 1
 #define RT_EXP_PORTABLE 2
@@ -317,11 +317,7 @@ int rt_last_kernel_ms(rt_context *ctx, double *ms_out);
  * generic kernel. Output is bit-identical either way; the one-off compile
  * (seconds, cached per process) pays off for scenes rendered many times.
  * Returns RT_E_DEVICE with the compiler log if hipRTC is unavailable or fails.
- * Takes effect immediately for the current scene and in every rt_set_scene.
- * enable == RT_SPECIALIZE_ASYNC (ABI 5): the compile runs on a background
- * thread and never blocks a call; launches use the generic kernel until it is
- * done (rt_render's cached context works this way). */
-#define RT_SPECIALIZE_ASYNC 2
+ * Takes effect immediately for the current scene and in every rt_set_scene. */
 int rt_set_specialize(rt_context *ctx, int enable);
 
 /* Acceleration of the exact search (MI355X-specific; pixels and counters are
@@ -442,11 +438,11 @@ int rt_ssim_rgba8(rt_context *ctx, const uint8_t *d_a, const uint8_t *d_b, int w
 /* Convenience, synchronous whole-frame Render() into host memory
  * (width*height*4 bytes, caller-owned): the replacement of
  * func Render(*Scene) image.Image (raytracer.go:589-682). Uses a cached
- * context and device frame buffer per device; scene specialisation in the
- * background (RT_SPECIALIZE_ASYNC: the first calls with a new scene shape run
- * the generic kernel, later ones the compiled variant; RT_RENDER_SPECIALIZE=0
- * in the environment turns it off). stats may be NULL. Includes the scene
- * upload and the PCIe transfer of the image. */
+ * context and device frame buffer per device, with scene specialisation
+ * (rt_set_specialize: the first call with a new scene shape pays the hipRTC
+ * compile, later ones reuse it; RT_RENDER_SPECIALIZE=0 in the environment
+ * keeps the generic kernel). stats may be NULL. Includes the scene upload and
+ * the PCIe transfer of the image. */
 int rt_render(const rt_scene *scene, uint8_t *rgba_out, rt_stats *stats);
 
 #ifdef __cplusplus

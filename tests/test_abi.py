@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt.load_library()
     for n in declared_functions():
         assert hasattr(lib, n), n
-    assert lib.rt_abi_version() == rt.abi.RT_ABI_VERSION == 5
+    assert lib.rt_abi_version() == rt.abi.RT_ABI_VERSION == 4
 
 
 def test_struct_layout_matches_header(tmp_path):

@@ -548,37 +548,11 @@ def test_specialised_full_4k_c3_equals_generic(ctx, spec_ctx):
     assert spec_ctx.specialized() == (True, 0.0)  # cached: no second compile
 
 
-def test_async_specialisation_equals_oracle():
-    """rt_set_specialize(RT_SPECIALIZE_ASYNC): the generic kernel until the
-    background compile is done, then the specialised one; every frame equals
-    the oracle (bytes + counters) whichever kernel rendered it."""
-    import time
-    packed = rt.scene.convert(rt.configs.c3(width=96, height=64))
-    ref, ost = oracle_bind.render_rows(packed)
-    c = rt.RenderContext(0, specialize="async")
-    try:
-        kernels = []
-        t_end = time.time() + 120
-        while True:
-            img, st = render(c, packed)  # (set_scene every time, as rt_render does)
-            assert_same(img, ref, "async specialisation")
-            assert st.as_dict() == ost.as_dict()
-            kernels.append(bool(c.specialized()[0]))
-            if kernels[-1] or time.time() > t_end:
-                break
-            time.sleep(0.1)
-        assert kernels[-1], "the background compile never finished"
-        img, st = render(c, packed)
-        assert_same(img, ref, "async specialisation (compiled)")
-    finally:
-        c.close()
-
-
 def test_rt_render_repeated_calls_equal_oracle():
     """rt_render (the synchronous Render() seam, raytracer.go:589) called
     repeatedly from one process on alternating scenes: cached context and
-    frame buffer, background specialisation -- every image and counter set
-    equal to the oracle's."""
+    frame buffer, specialised kernels from the process cache -- every image and
+    counter set equal to the oracle's."""
     import ctypes
     lib = rt.render.load_library()
     scenes = [rt.scene.convert(rt.configs.c3(width=80, height=48)),
