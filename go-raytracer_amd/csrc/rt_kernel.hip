@@ -344,7 +344,8 @@ struct BvhBuild {
         leaf_geo.insert(leaf_geo.end(), geo->begin() + (size_t)i * GEO, geo->begin() + (size_t)(i + 1) * GEO);
         int* gi = reinterpret_cast<int*>(&leaf_geo[leaf_geo.size() - GEO + 14]);
         gi[0] = i;
-        gi[1] = 0;
+        // scale + translation sphere: the kernel may take the diagonal transform (rt_render.h axis_o)
+        gi[1] = (*kind)[i] == RT_SPHERE && axis_sphere(&(*geo)[(size_t)i * GEO]) ? 1 : 0;
         gi[2] = (*kind)[i];
         gi[3] = 0;
       }
@@ -828,9 +829,16 @@ int spec_compile(const SpecKey& sk, double* ms) {
   if (sk.quads == SCH_PAIRS) defs.push_back("-DRT_PAIRS=1");
   std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
   for (const auto& d : defs) opts.push_back(d.c_str());
-  // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only)
+  // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only);
+  // RT_JIT_DEFS: the same, baked into an A/B build of the library
   std::vector<std::string> extra;
-  if (const char* e = getenv("RT_SPEC_EXTRA_FLAGS")) {
+#ifdef RT_JIT_DEFS
+  const char* baked = RT_JIT_DEFS;
+#else
+  const char* baked = nullptr;
+#endif
+  for (const char* e : {baked, (const char*)getenv("RT_SPEC_EXTRA_FLAGS")}) {
+    if (!e) continue;
     std::string cur;
     for (const char* q = e;; q++) {
       if (*q == ' ' || *q == 0) {
@@ -1226,6 +1234,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     if (o.kind == RT_PLANE) {
       double nw[3], dv;
       plane_consts(w2o, o.plane_point, o.plane_normal, nw, &dv);
+
       g[12] = o.plane_normal[0];
       g[13] = o.plane_normal[1];
       g[14] = o.plane_normal[2];

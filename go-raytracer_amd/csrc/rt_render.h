@@ -83,6 +83,10 @@
 #else
 #define CULL_AND(a, b) ((a) && (b))
 #endif
+#ifndef RT_AXIS_LEAF
+#define RT_AXIS_LEAF 0  // BVH leaves' scale + translation spheres take the diagonal transform (exact, see axis_o);
+                        // measured: C4 +3 % (a branch per leaf object, more spills), C5 within noise: off
+#endif
 #ifndef RT_CUBE_FAST
 #define RT_CUBE_FAST 1  // axis-aligned cube faces (bit-identical, see cube_hit)
 #endif
@@ -336,6 +340,9 @@ struct LeafRec {
   RecN<12> R;
   float cx, cy, cz, cr;
   int i, k;
+#if RT_AXIS_LEAF
+  bool ax;  // a scale + translation sphere (host: axis_sphere)
+#endif
 };
 __device__ __forceinline__ LeafRec ld_leaf(const double* base, int j) {
   const cdptr p = (cdptr)base + (size_t)j * 16;
@@ -346,7 +353,11 @@ __device__ __forceinline__ LeafRec ld_leaf(const double* base, int j) {
   L.cy = __int_as_float((int)(uint32_t)(b0 >> 32));
   L.cz = __int_as_float((int)(uint32_t)b1);
   L.cr = __int_as_float((int)(uint32_t)(b1 >> 32));
-  L.i = (int)(uint32_t)(uint64_t)__double_as_longlong(p[14]);
+  const uint64_t b2 = (uint64_t)__double_as_longlong(p[14]);
+  L.i = (int)(uint32_t)b2;
+#if RT_AXIS_LEAF
+  L.ax = (uint32_t)(b2 >> 32) != 0;
+#endif
   L.k = (int)(uint32_t)(uint64_t)__double_as_longlong(p[15]);
   return L;
 }
@@ -2380,6 +2391,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
         }
         const F3 idf = f3_rcp(df);
+#if RT_AXIS_LEAF
+        // leaves' scale + translation spheres take the diagonal transform (exact, see axis_o)
+        const bool rax = wave_all(!tr || (axis_o_ok(ray.o) && axis_d_ok(ray.d)));
+#endif
 #ifdef RT_PHASE_TIMING
         bd_trays++;
 #endif
@@ -2408,6 +2423,26 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
               const bool test = may_hit_s(act, of, df, tmax, L.cx, L.cy, L.cz, L.cr, slack);
               if (!wave_any(test)) continue;
+#if RT_AXIS_LEAF
+              if (spec_kind(RT_SPHERE) && L.k == RT_SPHERE && L.ax && rax) {
+                // scale + translation sphere: diagonal transform (exact, see axis_o)
+                EXDIAG(RT_SPHERE, 0, test);
+                if (test) {
+                  const double a[6] = {L.R.m[0], L.R.m[3], L.R.m[5], L.R.m[7], L.R.m[10], L.R.m[11]};
+                  Ray l;
+                  l.o = axis_o(a, ray.o);
+                  l.d = axis_d(a, ray.d);
+                  double t;
+                  if (sphere_hit(l, t) && (!found || t < best_t || (t == best_t && L.i < best_i))) {
+                    found = true;
+                    best_t = t;
+                    best_i = L.i;
+                    best_f = 0;
+                  }
+                }
+                continue;
+              }
+#endif
               trace_exact(L.i, L.k, L.R.m, test);
             }
           } else {
@@ -3002,6 +3037,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           shadow_obj(i, S.kind[i], S.geo + (size_t)i * GEO, hit);
         }
         const F3 sidf = f3_rcp(sdf);
+#if RT_AXIS_LEAF
+        const bool sax = wave_all(!hit || (axis_o_ok(sr.o) && axis_d_ok(sr.d)));
+#endif
 #ifdef RT_PHASE_TIMING
         bd_srays++;
 #endif
@@ -3029,6 +3067,21 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               const bool test = may_hit_s(CULL_AND(CULL_AND(act, L.i != hit_i), L.i < occ), sof, sdf, stmax, L.cx,
                                           L.cy, L.cz, L.cr, sslack);
               if (!wave_any(test)) continue;
+#if RT_AXIS_LEAF
+              if (spec_kind(RT_SPHERE) && L.k == RT_SPHERE && L.ax && sax) {
+                // scale + translation sphere: diagonal transform (exact, see axis_o)
+                EXDIAG(RT_SPHERE, 1, test);
+                if (test) {
+                  const double a[6] = {L.R.m[0], L.R.m[3], L.R.m[5], L.R.m[7], L.R.m[10], L.R.m[11]};
+                  Ray l;
+                  l.o = axis_o(a, sr.o);
+                  l.d = axis_d(a, sr.d);
+                  double t;
+                  if (sphere_hit(l, t) && t * rlen < dist) occ = L.i;
+                }
+                continue;
+              }
+#endif
               shadow_exact(L.i, L.k, L.R.m, test);
             }
           } else {

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--specialize", type=int, default=1, help="rt_set_specialize on each context (default 1)")
+    ap.add_argument("--frames", type=int, default=3, help="serial frames per variant per round")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     pkg = load_package()
@@ -51,6 +53,8 @@ def main():
         l.rt_last_error.restype = C.c_char_p
         h = C.c_void_p()
         assert l.rt_create(0, C.byref(h)) == 0, l.rt_last_error()
+        l.rt_set_specialize.argtypes = [C.c_void_p, C.c_int]
+        assert l.rt_set_specialize(h, a.specialize) == 0, l.rt_last_error()
         assert l.rt_set_scene(h, packed.ref()) == 0, l.rt_last_error()
         ctxs.append((path, l, h))
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
@@ -62,19 +66,20 @@ def main():
         for path, l, h in ctxs:
             st = pkg.abi.rt_stats()
             l.rt_read_stats(h, C.c_void_p(stream.cuda_stream), 1, C.byref(st))
-            out.zero_()
-            assert l.rt_render_rows_async(h, 0, H, C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)) == 0
-            ms = C.c_double()
-            l.rt_last_kernel_ms(h, C.byref(ms))
+            for _f in range(a.frames):
+                out.zero_()
+                assert l.rt_render_rows_async(h, 0, H, C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)) == 0
+                ms = C.c_double()
+                l.rt_last_kernel_ms(h, C.byref(ms))
+                if r > 0:
+                    times[path].append(ms.value)
             l.rt_read_stats(h, C.c_void_p(stream.cuda_stream), 1, C.byref(st))
             img = out.cpu()
             if ref is None:
                 ref = img.clone()
             elif not torch.equal(img, ref):
                 print("MISMATCH", path, int((img != ref).any(-1).sum()), "pixels", flush=True)
-            if r > 0:
-                times[path].append(ms.value)
-            rays[path] = st.total_rays()
+            rays[path] = st.total_rays() // a.frames
     res = []
     for path, _, _ in ctxs:
         t = sorted(times[path])
