@@ -52,16 +52,16 @@
 #include "../../include/rt_abi.h"
 #include "rt_device.h"
 
-// The generic kernels (every scene flavour, every feature, run-time object
-// loops) get 2 waves/SIMD: at 3 (168 VGPRs) they spilled ~175 VGPRs and
-// ~110 SGPRs to scratch, and one build of that spill-heavy code rendered the
-// deep-glass tiles of C4 wrong in the serial-sample schedule while unrelated
-// source changes (an unused branch, the frame prefetch switched off) made it
-// right again -- code no test could trust. The specialised kernels (hipRTC,
-// RT_MIN_WAVES from rt_render.h) fit 3 waves without spilling.
-#ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 2
-#endif
+// The generic kernels run at 3 waves/SIMD like the specialised ones
+// (RT_MIN_WAVES from rt_render.h). Round 3 had dropped them to 2 after a
+// build rendered 14 deep-glass tiles of a reduced C4 frame wrong in the
+// serial-sample schedule; rebuilding that tree at 3 waves with each of its two
+// candidate fixes (profiles/r04/generic/) reproduced the failure exactly
+// without the fixes and with the t0/t1 initialisation alone, and removed it
+// with the BVH stack push from every active lane (WaveStack::push) alone: a
+// push written by lane 0 only was lost whenever lane 0 was inactive there.
+// At 3 waves the generic C3 kernel takes 4.61 ms instead of 5.51 (C2 0.44
+// instead of 0.49), GPU suite green.
 #include "rt_render.h"
 #include "rt_jit_src.inc"
 
@@ -455,6 +455,56 @@ struct BvhBuild {
     ni[3] = rr.minidx;
     out.ref = node << 3;
     return out;
+  }
+
+  // 4-wide BVH (rt_render.h RT_BVH4): node `ref` of the binary tree collapsed
+  // one level -- its children are its binary children's children, or the
+  // binary child itself when that is a leaf -- into nodes4 ([m][BN4]: boxes
+  // SoA, refs, smallest indices; children in ascending smallest index, empty
+  // slots ref -1). Leaf refs are unchanged. Returns the new ref; depth4 and
+  // stack4 (most stack entries a traversal can hold) follow the tree.
+  std::vector<float> nodes4;
+  int depth4 = 0, stack4 = 0;
+  int collapse(int ref, int depth, int pending) {
+    if (ref & 7) return ref;
+    depth4 = std::max(depth4, depth);
+    struct Ch {
+      const float* box;
+      int ref, mn;
+    };
+    Ch ch[4];
+    int n = 0;
+    const float* nb = &nodes[(size_t)(ref >> 3) * BN];
+    const int* ni = reinterpret_cast<const int*>(nb + 12);
+    for (int s = 0; s < 2; s++) {
+      if (ni[s] & 7) {
+        ch[n++] = {nb + 6 * s, ni[s], ni[2 + s]};
+      } else {
+        const float* cb = &nodes[(size_t)(ni[s] >> 3) * BN];
+        const int* ci = reinterpret_cast<const int*>(cb + 12);
+        for (int t = 0; t < 2; t++) ch[n++] = {cb + 6 * t, ci[t], ci[2 + t]};
+      }
+    }
+    std::sort(ch, ch + n, [](const Ch& a, const Ch& b) { return a.mn < b.mn; });
+    const int m = (int)(nodes4.size() / BN4);
+    nodes4.resize(nodes4.size() + BN4, 0.0f);
+    // a traversal here holds the entries pending above plus up to n pushed
+    stack4 = std::max(stack4, pending + n);
+    int cref[4] = {-1, -1, -1, -1}, cmn[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+    float cbox[4][6] = {};
+    for (int c = 0; c < n; c++) {
+      cref[c] = collapse(ch[c].ref, depth + 1, pending + n - 1);
+      cmn[c] = ch[c].mn;
+      for (int k = 0; k < 6; k++) cbox[c][k] = ch[c].box[k];
+    }
+    float* q = &nodes4[(size_t)m * BN4];
+    int* qi = reinterpret_cast<int*>(q + 24);
+    for (int c = 0; c < 4; c++) {
+      for (int k = 0; k < 6; k++) q[4 * k + c] = cbox[c][k];
+      qi[c] = cref[c];
+      qi[4 + c] = cmn[c];
+    }
+    return m << 3;
   }
 };
 
@@ -1501,6 +1551,13 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       b.ord = bounded;
       b.build(0, (int)bounded.size(), 0);  // root: node 0 (> 4 objects)
       s.use_bvh = b.max_depth + 2 < BVH_STACK;
+#if RT_BVH4
+      if (s.use_bvh) {
+        b.collapse(0, 0, 0);  // root: node 0 of nodes4
+        b.nodes.swap(b.nodes4);
+        s.use_bvh = b.stack4 + 2 < BVH_STACK;
+      }
+#endif
     }
     if (!s.use_bvh) {
       b.nodes.clear();
@@ -1550,7 +1607,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       return rc;
     }
     s.nplanes = (int)planes.size();
-    s.nnodes = (int)(b.nodes.size() / BN);
+    s.nnodes = (int)(b.nodes.size() / (RT_BVH4 ? BN4 : BN));
   }
   // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
   int frames = std::max(1, s.depth - 1);
@@ -2013,6 +2070,13 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
         HIP_TRY(hipMemcpy(sh, c->stats + ST_SHDIAG, sizeof sh, hipMemcpyDeviceToHost));
         fprintf(stderr, "[share] posted samples %llu subtrees %llu, claims %llu, reclaims %llu, waits %llu, idle polls %llu\n",
                 sh[0], sh[1], sh[2], sh[3], sh[4], sh[5]);
+      }
+      {
+        unsigned long long pd[6];
+        HIP_TRY(hipMemcpy(pd, c->stats + ST_PASSDIAG, sizeof pd, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[passes] trace %llu (%.1f lanes), shade %llu (%.1f lanes), gen %llu (%.1f lanes)\n", pd[0],
+                (double)pd[1] / std::max(1ull, pd[0]), pd[2], (double)pd[3] / std::max(1ull, pd[2]), pd[4],
+                (double)pd[5] / std::max(1ull, pd[4]));
       }
       fprintf(stderr, "[waves] lifetime mean %.4g cycles, max %.4g cycles (mean/max %.3f)\n",
               (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches), (double)bd[7],
