@@ -74,6 +74,8 @@ def parse():
                    help="rt_set_schedule: how pixels are dealt to lanes (identical pixels and counters); "
                         "auto picks from depth, pixels per lane and frames in flight. The PMC passes run "
                         "--inflight 1 with the schedule the in-flight bench picks")
+    p.add_argument("--work-sharing", choices=["on", "off"], default="off",
+                   help="rt_set_work_sharing: tail work sharing compiled into the specialised kernel")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -176,10 +178,12 @@ def gpu_span_ms(evs):
     return span / len(evs)
 
 
-def make_contexts(pkg, dev, packed, n, specialize, accel=None, schedule="auto"):
+def make_contexts(pkg, dev, packed, n, specialize, accel=None, schedule="auto", sharing=False):
     ctxs = []
     for _ in range(n):
         c = pkg.RenderContext(dev.index, specialize=specialize)
+        if sharing:
+            c.set_work_sharing(True)
         if accel is not None:
             c.set_accel(accel)
         c.set_schedule({"auto": pkg.abi.RT_SCHED_AUTO, "pixel": pkg.abi.RT_SCHED_PIXEL,
@@ -318,7 +322,8 @@ def main():
     if args.inflight < 1:
         raise SystemExit("--inflight must be >= 1")
     ctxs = make_contexts(pkg, dev, packed, args.inflight, args.specialize == "on",
-                         accel=0 if args.accel == "none" else None, schedule=args.schedule)
+                         accel=0 if args.accel == "none" else None, schedule=args.schedule,
+                         sharing=args.work_sharing == "on")
     ctx = ctxs[0]
     spec_active, spec_ms = ctx.specialized()
     order_active, order_ms = ctx.tile_order_info()
@@ -404,6 +409,7 @@ def main():
                                       else "rows%d-%s%s" % (world, args.shard, "-pipelined" if dr.pipeline else ""),
                        "frames_in_flight": args.inflight,
                        "schedule": args.schedule,
+                       "work_sharing": args.work_sharing,
                        "kernel": "specialised" if spec_active else "generic",
                        "accel": "bvh+cull" if args.accel == "bvh" else "none (brute force)",
                        "spec_compile_ms": round(spec_ms, 1),

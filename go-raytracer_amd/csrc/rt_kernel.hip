@@ -1382,8 +1382,83 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     ci[0] = o.csg_first;
     ci[1] = o.csg_count;
     ci[2] = (int)mcode.size();
+    // leaf groups (rt_render.h csg_hit): header [ngroups, ngroups x (FP32
+    // bounding sphere of the members' padded spheres, 8 leaf indices as
+    // bytes)], then the membership program. Groups are spatial (median splits
+    // of the bounded leaves' centres, <= 8 leaves each; planes in groups of
+    // their own, never culled); small composites get none.
+    {
+      std::vector<std::vector<int>> groups;
+      std::vector<int> bounded_l, plane_l;
+      for (int j = 0; j < o.csg_count; j++)
+        (kind[s.nobj + o.csg_first + j] == RT_PLANE ? plane_l : bounded_l).push_back(j);
+      if (o.csg_count >= CSG_GROUP_MIN) {
+        std::function<void(std::vector<int>)> split = [&](std::vector<int> v) {
+          if (v.size() <= 8) {
+            groups.push_back(v);
+            return;
+          }
+          double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+          for (int j : v)
+            for (int q = 0; q < 3; q++) {
+              lo[q] = std::min(lo[q], bcen[(size_t)(s.nobj + o.csg_first + j) * 3 + q]);
+              hi[q] = std::max(hi[q], bcen[(size_t)(s.nobj + o.csg_first + j) * 3 + q]);
+            }
+          int ax = 0;
+          for (int q = 1; q < 3; q++)
+            if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
+          std::sort(v.begin(), v.end(), [&](int a, int b) {
+            const double ca = bcen[(size_t)(s.nobj + o.csg_first + a) * 3 + ax],
+                         cb = bcen[(size_t)(s.nobj + o.csg_first + b) * 3 + ax];
+            return ca < cb || (ca == cb && a < b);
+          });
+          const size_t half = (v.size() + 1) / 2;
+          split(std::vector<int>(v.begin(), v.begin() + half));
+          split(std::vector<int>(v.begin() + half, v.end()));
+        };
+        if (!bounded_l.empty()) split(bounded_l);
+        for (size_t q = 0; q < plane_l.size(); q += 8)
+          groups.push_back(std::vector<int>(plane_l.begin() + q, plane_l.begin() + std::min(plane_l.size(), q + 8)));
+      }
+      mcode.push_back((int)groups.size());
+      for (const auto& gv : groups) {
+        bool fin = true;
+        double c[3] = {0, 0, 0}, lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (int j : gv) {
+          const int li = s.nobj + o.csg_first + j;
+          if (kind[li] == RT_PLANE) fin = false;
+          for (int q = 0; q < 3; q++) {
+            lo[q] = std::min(lo[q], bcen[(size_t)li * 3 + q] - brad[li]);
+            hi[q] = std::max(hi[q], bcen[(size_t)li * 3 + q] + brad[li]);
+          }
+        }
+        for (int q = 0; q < 3; q++) c[q] = 0.5 * (lo[q] + hi[q]);
+        double rr = 0.0;
+        for (int j : gv) {
+          const int li = s.nobj + o.csg_first + j;
+          const double d = std::sqrt((bcen[(size_t)li * 3] - c[0]) * (bcen[(size_t)li * 3] - c[0]) +
+                                     (bcen[(size_t)li * 3 + 1] - c[1]) * (bcen[(size_t)li * 3 + 1] - c[1]) +
+                                     (bcen[(size_t)li * 3 + 2] - c[2]) * (bcen[(size_t)li * 3 + 2] - c[2]));
+          rr = std::max(rr, d + brad[li]);
+        }
+        float gf[4] = {(float)c[0], (float)c[1], (float)c[2],
+                       fin ? f_up(rr * 1.0001 + 1e-6 * (1.0 + std::fabs(c[0]) + std::fabs(c[1]) + std::fabs(c[2])))
+                           : std::numeric_limits<float>::infinity()};
+        int w[6];
+        std::memcpy(w, gf, sizeof gf);
+        uint32_t lb[2] = {0xffffffffu, 0xffffffffu};
+        for (size_t q = 0; q < gv.size(); q++) {
+          lb[q >> 2] &= ~(0xffu << (8 * (q & 3)));
+          lb[q >> 2] |= (uint32_t)gv[q] << (8 * (q & 3));
+        }
+        w[4] = (int)lb[0];
+        w[5] = (int)lb[1];
+        mcode.insert(mcode.end(), w, w + 6);
+      }
+    }
+    const int prog0 = (int)mcode.size();
     csg_mask_program(in->csg_code + o.csg_code, o.csg_code_len, mcode);
-    ci[3] = (int)mcode.size() - ci[2];
+    ci[3] = (int)mcode.size() - prog0;
     s.has_csg = true;
   }
   std::vector<double> mats((size_t)s.nmats * MAT, 0.0);

@@ -955,6 +955,11 @@ __device__ __forceinline__ void leaf_interval(int kind, const double* g, const R
 // groups of leaves collapsed into one mask test (bit stacks, depth <=
 // RT_CSG_MAX_LEAVES).
 enum { RT_CSG_ANY = -4, RT_CSG_ALL = -5 };
+// composites with at least this many leaves get spatial leaf groups (host)
+#ifndef RT_CSG_GROUP_MIN
+#define RT_CSG_GROUP_MIN 16
+#endif
+enum { CSG_GROUP_MIN = RT_CSG_GROUP_MIN };
 __device__ __forceinline__ bool csg_eval(const int* code, int n, uint64_t m0, uint64_t m1) {
   uint64_t st0 = 0, st1 = 0;
   int sp = 0;
@@ -997,7 +1002,7 @@ __device__ __forceinline__ bool csg_hit_all(const double* geo, const int* kinds,
                                             double cut_lim, bool cut_strict) {
   const int* ci = reinterpret_cast<const int*>(g + 14);
   const int first = nobj + ci[0], count = ci[1];
-  const int* prog = code + ci[2];
+  const int* prog = code + ci[2] + 1 + 6 * code[ci[2]];  // past the leaf groups (csg_hit)
   const int plen = ci[3];
   double A[RT_CSG_MAX_LEAVES], B[RT_CSG_MAX_LEAVES];
   int F[RT_CSG_MAX_LEAVES];
@@ -1098,7 +1103,12 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
   if constexpr (RT_CSG_LIVE == 0) return csg_hit_all(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
   const int* ci = reinterpret_cast<const int*>(g + 14);
   const int first = nobj + ci[0], count = ci[1];
-  const int* prog = code + ci[2];
+  // leaf groups (host: spatial, <= 8 leaves, FP32 bounding sphere): a group
+  // no lane's ray can reach is skipped as a whole; the live list then fills
+  // out of leaf order, so the search below breaks ties on the leaf index
+  const int* hdr = code + ci[2];
+  const int ngroups = hdr[0];
+  const int* prog = hdr + 1 + 6 * ngroups;
   const int plen = ci[3];
   const F3 of = f3(r.o), df = f3(r.d);
   const float slack = ray_slack(of);
@@ -1110,10 +1120,10 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
     LF[s] = 0;
   }
   int n = 0;
-  for (int j = 0; j < count; j++) {
+  auto add_leaf = [&](int j) {
     const int k = kinds[first + j];
     const double* lg = geo + (size_t)(first + j) * GEO;
-    if (k != RT_PLANE && !may_hit(of, df, 3.0e38f, lg, slack)) continue;
+    if (k != RT_PLANE && !may_hit(of, df, 3.0e38f, lg, slack)) return;
     double a, b;
     int f;
     leaf_interval(k, lg, r, a, b, f);
@@ -1127,6 +1137,24 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
         }
       n++;
     }
+  };
+  if (ngroups == 0) {
+    for (int j = 0; j < count; j++) add_leaf(j);
+  } else {
+    for (int q = 0; q < ngroups; q++) {
+      const int* gr = hdr + 1 + 6 * q;
+      const bool gh = may_hit_s(true, of, df, 3.0e38f, __int_as_float(gr[0]), __int_as_float(gr[1]),
+                                __int_as_float(gr[2]), __int_as_float(gr[3]), slack);
+      if (!wave_any(gh)) continue;
+      if (gh) {
+        const uint32_t w0 = (uint32_t)gr[4], w1 = (uint32_t)gr[5];
+        for (int e = 0; e < 8; e++) {
+          const int j = (int)(((e < 4 ? w0 : w1) >> (8 * (e & 3))) & 0xffu);
+          if (j == 0xff) break;
+          add_leaf(j);
+        }
+      }
+    }
   }
 #ifdef RT_CSG_DIAG
   atomicAdd(RT_CSG_DIAG + 0, 1ull);  // composite searches
@@ -1137,19 +1165,24 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
   double tc = 0.0;
   for (;;) {
     double te = __builtin_inf();
-    int se = -1, jend = 0;
+    int se = -1, jend = 0, je = 0x7fffffff;
 #pragma unroll
     for (int s = 0; s < K; s++) {
       if (s < n) {
-        if (LA[s] > tc && LA[s] < te) {
+        // the first end point past tc; ties: the lowest leaf, then its entry
+        // (what csg_hit_all's scan in leaf order gives)
+        const int lj = LF[s] & 0xff;
+        if (LA[s] > tc && (LA[s] < te || (LA[s] == te && lj < je))) {
           te = LA[s];
           se = s;
           jend = 0;
+          je = lj;
         }
-        if (LB[s] > tc && LB[s] < te) {
+        if (LB[s] > tc && (LB[s] < te || (LB[s] == te && lj < je))) {
           te = LB[s];
           se = s;
           jend = 1;
+          je = lj;
         }
       }
     }
