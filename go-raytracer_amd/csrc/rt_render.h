@@ -288,15 +288,18 @@ struct Ray {
 
 // rayToObjectSpace (raytracer.go:51-56) with prim.Mat4.MulPoint/MulDir
 // (vec.go:298-313): m points at the 3x4 affine rows.
-__device__ __forceinline__ d3 to_obj_o(const double* m, d3 o) {  // MulPoint (vec.go:298-304)
+template <typename MP>
+__device__ __forceinline__ d3 to_obj_o(MP m, d3 o) {  // MulPoint (vec.go:298-304)
   return mk(m[0] * o.x + m[1] * o.y + m[2] * o.z + m[3], m[4] * o.x + m[5] * o.y + m[6] * o.z + m[7],
             m[8] * o.x + m[9] * o.y + m[10] * o.z + m[11]);
 }
-__device__ __forceinline__ d3 to_obj_d(const double* m, d3 d) {  // MulDir (vec.go:307-313)
+template <typename MP>
+__device__ __forceinline__ d3 to_obj_d(MP m, d3 d) {  // MulDir (vec.go:307-313)
   return mk(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
             m[8] * d.x + m[9] * d.y + m[10] * d.z);
 }
-__device__ __forceinline__ Ray to_obj(const double* m, const Ray& r) {
+template <typename MP>
+__device__ __forceinline__ Ray to_obj(MP m, const Ray& r) {
   Ray l;
   l.o = to_obj_o(m, r.o);
   l.d = to_obj_d(m, r.d);
@@ -331,6 +334,11 @@ __device__ __forceinline__ d3 axis_d(const double* a, d3 d) { return mk(a[0] * d
 typedef const __attribute__((address_space(4))) double* cdptr;
 typedef const __attribute__((address_space(4))) float* cfptr;
 typedef const __attribute__((address_space(4))) int* ciptr;
+// the FP32 words of a double record, in the record's address space
+__device__ __forceinline__ const float* as_f(const double* p) { return reinterpret_cast<const float*>(p); }
+__device__ __forceinline__ cfptr as_f(cdptr p) { return (cfptr)p; }
+__device__ __forceinline__ const int* as_i(const double* p) { return reinterpret_cast<const int*>(p); }
+__device__ __forceinline__ ciptr as_i(cdptr p) { return (ciptr)p; }
 template <int N>
 struct RecN {
   double m[N];
@@ -345,6 +353,20 @@ __device__ __forceinline__ RecN<N> ld_rec(cdptr p) {
   for (int q = 0; q < N; q++) r.m[q] = p[q];
   return r;
 }
+// Specialised LDS scenes: object i's geo record (GEO doubles) through scalar
+// loads from the global blob instead of LDS (RT_SPEC_SGEO): the loop over
+// objects is unrolled, so the record lands in SGPRs and feeds the culls and
+// the FP64 transform as scalar operands (C3 spec: LDS reads 266 -> 106 in the
+// ISA; same-box serial frames C3 -3.0 %, c3cone -2.1 %, C2 -1.7 %,
+// profiles/r04/sgeo/). RT_SPEC_SLIGHTS does the same for the lights, the
+// frame constants and the plane culls' records (all kernels): no further gain
+// on C3, c4csg +1.5 % -- off.
+#ifndef RT_SPEC_SGEO
+#define RT_SPEC_SGEO 1
+#endif
+#ifndef RT_SPEC_SLIGHTS
+#define RT_SPEC_SLIGHTS 0
+#endif
 // A BVH leaf object's record (bvh_geo: GEO doubles in leaf order; 0..11
 // WorldToObject, 12..13 the FP32 bounding sphere, 14 index, 15 kind) read
 // through the constant address space: the index is wave-uniform, so this is
@@ -745,8 +767,9 @@ struct F3 {
 __device__ __forceinline__ F3 f3(d3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
 // `slack` (ray_slack) widens the radius by the FP32 rounding scale of the
 // ray origin, so origins far from the object stay conservative.
-__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, const double* g, float slack) {
-  const float* b = reinterpret_cast<const float*>(g + 12);
+template <typename DP>
+__device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, DP g, float slack) {
+  const auto b = as_f(g + 12);
   // (fused multiply-adds: only less rounding than the bound allows for)
   float ox = b[0] - o.x, oy = b[1] - o.y, oz = b[2] - o.z;
   float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
@@ -841,6 +864,28 @@ struct WaveStack {
     sp++;
   }
 };
+// Binary BVH step with the first child kept in registers (RT_BVH_CONT): the
+// child the stack order would pop next is visited directly and only the other
+// is pushed, so a descent skips the LDS store and reload between a node and
+// its first child. Nodes are visited in the same order as with two pushes.
+#ifndef RT_BVH_CONT
+#define RT_BVH_CONT 0
+#endif
+__device__ __forceinline__ void bvh_next(WaveStack& st, int& sp, int lane, bool c1_first, int r0, int r1, uint64_t m0,
+                                         uint64_t m1, int& nr, uint64_t& nm, bool& have) {
+  const int fr = c1_first ? r1 : r0, sr = c1_first ? r0 : r1;
+  const uint64_t fm = c1_first ? m1 : m0, sm = c1_first ? m0 : m1;
+  if (fm) {
+    if (sm) st.push(sp, lane, sr, sm);
+    nr = fr;
+    nm = fm;
+    have = true;
+  } else if (sm) {
+    nr = sr;
+    nm = sm;
+    have = true;
+  }
+}
 __device__ __forceinline__ F3 f3_rcp(F3 d) {
   return F3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
 }
@@ -849,7 +894,8 @@ __device__ __forceinline__ F3 f3_rcp(F3 d) {
 // csg_member, csg_intersect restate the same semantics op for op) ----
 // One convex leaf's interval [a, b] along the ray and the faces it enters /
 // leaves by: f = fa | fb << 4 | 256 when non-empty.
-__device__ __forceinline__ void leaf_interval(int kind, const double* g, const Ray& r, double& a, double& b, int& f) {
+template <typename DP>
+__device__ __forceinline__ void leaf_interval(int kind, DP g, const Ray& r, double& a, double& b, int& f) {
   const Ray l = to_obj(g, r);
   a = -__builtin_inf();
   b = __builtin_inf();
@@ -960,7 +1006,16 @@ enum { RT_CSG_ANY = -4, RT_CSG_ALL = -5 };
 #define RT_CSG_GROUP_MIN 16
 #endif
 enum { CSG_GROUP_MIN = RT_CSG_GROUP_MIN };
-__device__ __forceinline__ bool csg_eval(const int* code, int n, uint64_t m0, uint64_t m1) {
+// The composite search's wave-uniform reads (postfix program, leaf groups,
+// leaf kinds and records) through scalar loads from the global blob instead
+// of LDS (c4csg serial, same box: 15.33 -> 14.68 ms; the composite's fields
+// made wave-uniform with readfirstlane first: 16.32 -> 15.33 ms, VGPR spills
+// of the CSG quads kernel 95 -> 60; profiles/r04/csg/ab_c4csg_scalar.log)
+#ifndef RT_CSG_SCALAR
+#define RT_CSG_SCALAR 1
+#endif
+template <typename IP>
+__device__ __forceinline__ bool csg_eval(IP code, int n, uint64_t m0, uint64_t m1) {
   uint64_t st0 = 0, st1 = 0;
   int sp = 0;
   auto get = [&](int i) -> bool { return ((i < 64 ? st0 >> i : st1 >> (i - 64)) & 1) != 0; };
@@ -997,12 +1052,13 @@ __device__ __forceinline__ bool csg_eval(const int* code, int n, uint64_t m0, ui
 // (strictly beyond, or at-or-beyond when !cut_strict): the caller cannot use
 // such a hit (closest hit: t > best; shadow: t * |d| >= dist), so stopping
 // there changes no result.
-__device__ __forceinline__ bool csg_hit_all(const double* geo, const int* kinds, const int* code, int nobj,
-                                            const double* g, const Ray& r, double& t, int& face, double cut_m,
+template <typename DP, typename IP, typename GP>
+__device__ __forceinline__ bool csg_hit_all(DP geo, IP kinds, IP code, int nobj,
+                                            GP g, const Ray& r, double& t, int& face, double cut_m,
                                             double cut_lim, bool cut_strict) {
-  const int* ci = reinterpret_cast<const int*>(g + 14);
+  const auto ci = as_i(g + 14);
   const int first = nobj + ci[0], count = ci[1];
-  const int* prog = code + ci[2] + 1 + 6 * code[ci[2]];  // past the leaf groups (csg_hit)
+  const auto prog = code + ci[2] + 1 + 6 * code[ci[2]];  // past the leaf groups (csg_hit)
   const int plen = ci[3];
   double A[RT_CSG_MAX_LEAVES], B[RT_CSG_MAX_LEAVES];
   int F[RT_CSG_MAX_LEAVES];
@@ -1014,7 +1070,7 @@ __device__ __forceinline__ bool csg_hit_all(const double* geo, const int* kinds,
   uint64_t live0 = 0, live1 = 0;  // leaves with a non-empty interval, in registers
   for (int j = 0; j < count; j++) {
     const int k = kinds[first + j];
-    const double* lg = geo + (size_t)(first + j) * GEO;
+    const auto lg = geo + (size_t)(first + j) * GEO;
     if (k != RT_PLANE && !may_hit(of, df, 3.0e38f, lg, slack)) continue;
     leaf_interval(k, lg, r, A[j], B[j], F[j]);
     if (F[j] & 256) {
@@ -1091,25 +1147,29 @@ __device__ unsigned long long g_csg_diag[4];  // diagnostic build: searches, ove
 #ifndef RT_CSG_LIVE
 #define RT_CSG_LIVE 6  // 0: always the scratch-array search
 #endif
-__device__ __forceinline__ bool csg_hit_all_call(const double* geo, const int* kinds, const int* code, int nobj,
-                                              const double* g, const Ray& r, double& t, int& face, double cut_m,
+template <typename DP, typename IP, typename GP>
+__device__ __forceinline__ bool csg_hit_all_call(DP geo, IP kinds, IP code, int nobj,
+                                              GP g, const Ray& r, double& t, int& face, double cut_m,
                                               double cut_lim, bool cut_strict) {
   return csg_hit_all(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
 }
-__device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, const int* code, int nobj,
-                                        const double* g, const Ray& r, double& t, int& face, double cut_m = 1.0,
+template <typename DP, typename IP, typename GP>
+__device__ __forceinline__ bool csg_hit(DP geo, IP kinds, IP code, int nobj,
+                                        GP g, const Ray& r, double& t, int& face, double cut_m = 1.0,
                                         double cut_lim = __builtin_inf(), bool cut_strict = true) {
   constexpr int K = RT_CSG_LIVE > 0 ? RT_CSG_LIVE : 1;
   if constexpr (RT_CSG_LIVE == 0) return csg_hit_all(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
-  const int* ci = reinterpret_cast<const int*>(g + 14);
-  const int first = nobj + ci[0], count = ci[1];
+  const auto ci = as_i(g + 14);
+  // (the composite's fields are wave-uniform: readfirstlane keeps the reads
+  // below them scalar)
+  const int first = __builtin_amdgcn_readfirstlane(nobj + ci[0]), count = __builtin_amdgcn_readfirstlane(ci[1]);
   // leaf groups (host: spatial, <= 8 leaves, FP32 bounding sphere): a group
   // no lane's ray can reach is skipped as a whole; the live list then fills
   // out of leaf order, so the search below breaks ties on the leaf index
-  const int* hdr = code + ci[2];
-  const int ngroups = hdr[0];
-  const int* prog = hdr + 1 + 6 * ngroups;
-  const int plen = ci[3];
+  const auto hdr = code + __builtin_amdgcn_readfirstlane(ci[2]);
+  const int ngroups = __builtin_amdgcn_readfirstlane(hdr[0]);
+  const auto prog = hdr + 1 + 6 * ngroups;
+  const int plen = __builtin_amdgcn_readfirstlane(ci[3]);
   const F3 of = f3(r.o), df = f3(r.d);
   const float slack = ray_slack(of);
   double LA[K], LB[K];
@@ -1122,7 +1182,7 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
   int n = 0;
   auto add_leaf = [&](int j) {
     const int k = kinds[first + j];
-    const double* lg = geo + (size_t)(first + j) * GEO;
+    const auto lg = geo + (size_t)(first + j) * GEO;
     if (k != RT_PLANE && !may_hit(of, df, 3.0e38f, lg, slack)) return;
     double a, b;
     int f;
@@ -1142,12 +1202,13 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
     for (int j = 0; j < count; j++) add_leaf(j);
   } else {
     for (int q = 0; q < ngroups; q++) {
-      const int* gr = hdr + 1 + 6 * q;
+      const auto gr = hdr + 1 + 6 * q;
       const bool gh = may_hit_s(true, of, df, 3.0e38f, __int_as_float(gr[0]), __int_as_float(gr[1]),
                                 __int_as_float(gr[2]), __int_as_float(gr[3]), slack);
       if (!wave_any(gh)) continue;
       if (gh) {
-        const uint32_t w0 = (uint32_t)gr[4], w1 = (uint32_t)gr[5];
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane(gr[4]),
+                       w1 = (uint32_t)__builtin_amdgcn_readfirstlane(gr[5]);
         for (int e = 0; e < 8; e++) {
           const int j = (int)(((e < 4 ? w0 : w1) >> (8 * (e & 3))) & 0xffu);
           if (j == 0xff) break;
@@ -1233,16 +1294,18 @@ __device__ __forceinline__ bool csg_hit(const double* geo, const int* kinds, con
 struct PlaneO {
   float f0, a0;
 };
-__device__ __forceinline__ PlaneO may_hit_plane_o(F3 o, const double* sh) {
-  const float* c = reinterpret_cast<const float*>(sh + 16);
+template <typename DP>
+__device__ __forceinline__ PlaneO may_hit_plane_o(F3 o, DP sh) {
+  const auto c = as_f(sh + 16);
   PlaneO r;
   r.f0 = __builtin_fmaf(c[0], o.x, __builtin_fmaf(c[1], o.y, __builtin_fmaf(c[2], o.z, c[3])));
   r.a0 = __builtin_fmaf(c[4], __builtin_fabsf(o.x),
                         __builtin_fmaf(c[5], __builtin_fabsf(o.y), __builtin_fmaf(c[6], __builtin_fabsf(o.z), c[7])));
   return r;
 }
-__device__ __forceinline__ bool may_hit_plane_d(PlaneO po, F3 d, float tmax, const double* sh) {
-  const float* c = reinterpret_cast<const float*>(sh + 16);
+template <typename DP>
+__device__ __forceinline__ bool may_hit_plane_d(PlaneO po, F3 d, float tmax, DP sh) {
+  const auto c = as_f(sh + 16);
   const float f0 = po.f0, a0 = po.a0;
   const float sl = __builtin_fmaf(c[0], d.x, __builtin_fmaf(c[1], d.y, c[2] * d.z));
   const float a1 = __builtin_fmaf(c[4], __builtin_fabsf(d.x), __builtin_fmaf(c[5], __builtin_fabsf(d.y), c[6] * __builtin_fabsf(d.z)));
@@ -1258,7 +1321,8 @@ __device__ __forceinline__ bool may_hit_plane_d(PlaneO po, F3 d, float tmax, con
   }
   return !((f0 > m0 && f1 > m1) || (f0 < -m0 && f1 < -m1));
 }
-__device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, const double* sh) {
+template <typename DP>
+__device__ __forceinline__ bool may_hit_plane(F3 o, F3 d, float tmax, DP sh) {
   return may_hit_plane_d(may_hit_plane_o(o, sh), d, tmax, sh);
 }
 
@@ -1625,8 +1689,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   S.shade = reinterpret_cast<const double*>(base + P.off_shade);
   S.mats = reinterpret_cast<const double*>(base + P.off_mats);
   // lights section: a 16-double record of per-frame constants, then the lights
+#if RT_SPEC_SLIGHTS
+  const cdptr G = (cdptr)(blob + P.off_lights);
+  S.lights = reinterpret_cast<const double*>(base + P.off_lights) + GLOB;
+#else
   const double* G = reinterpret_cast<const double*>(base + P.off_lights);
   S.lights = G + GLOB;
+#endif
   S.kind = reinterpret_cast<const int*>(base + P.off_kind);
   S.objmat = reinterpret_cast<const int*>(base + P.off_objmat);
   S.pref = reinterpret_cast<const uint32_t*>(base + P.off_pref);
@@ -1634,6 +1703,30 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   S.code = reinterpret_cast<const uint32_t*>(base + P.off_code);
   S.entry = reinterpret_cast<const int*>(base + P.off_entry);
   S.consts = reinterpret_cast<const uint64_t*>(base + P.off_consts);
+#if RT_SPEC_SGEO && defined(RT_SPEC_NOBJ)
+  const cdptr sgeo = (cdptr)(blob + P.off_geo);  // object records through scalar loads
+#endif
+#if RT_CSG_SCALAR
+  // composite programs, leaf groups and leaf records through scalar loads
+  const cdptr cs_geo = (cdptr)(blob + P.off_geo);
+  const ciptr cs_kind = (ciptr)(blob + P.off_kind);
+  const ciptr cs_csg = (ciptr)(blob + P.off_csg);
+#define CSG_ARGS cs_geo, cs_kind, cs_csg
+#define CSG_G(i, g) (cs_geo + (size_t)(i) * GEO)
+#else
+#define CSG_ARGS S.geo, S.kind, S.csg
+#define CSG_G(i, g) (g)
+#endif
+#if RT_SPEC_SLIGHTS
+  // wave-uniform records through scalar loads: lights, plane culls
+  const cdptr slights = G + GLOB;
+  const cdptr sshade = (cdptr)(blob + P.off_shade);
+#define LTP(li) (slights + (size_t)(li) * LGT)
+#define SHP(i) (sshade + (size_t)(i) * SHD)
+#else
+#define LTP(li) (S.lights + (size_t)(li) * LGT)
+#define SHP(i) (S.shade + (size_t)(i) * SHD)
+#endif
 
   const int lane = (int)(threadIdx.x & 63);
   const int wslot = (int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
@@ -2365,7 +2458,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           int f;
           bool h;
           if constexpr (CSG)
-            h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, ray, t, f, 1.0,
+            h = k == RT_CSG ? csg_hit(CSG_ARGS, P.nobj, CSG_G(i, g), ray, t, f, 1.0,
                                       found ? best_t : __builtin_inf(), true)
                             : object_hit(k, g, ray, t, f);
           else
@@ -2386,7 +2479,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         // an object entered beyond the lane's current best cannot win (strict <)
         const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
         test = k != RT_PLANE ? may_hit_a(test, of, df, tmax, g, slack)
-                             : CULL_AND(test, may_hit_plane(of, df, tmax, S.shade + (size_t)i * SHD));
+                             : CULL_AND(test, may_hit_plane(of, df, tmax, SHP(i)));
         if (!wave_any(test)) return;
 #endif
         trace_exact(i, k, g, test);
@@ -2395,7 +2488,17 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #ifdef RT_SPEC_NOBJ
         {
 #pragma unroll
-          for (int i = 0; i < RT_SPEC_NOBJ; i++) trace_obj(i, spec_kinds[i], S.geo + (size_t)i * GEO, tr);
+          for (int i = 0; i < RT_SPEC_NOBJ; i++) {
+#if RT_SPEC_SGEO
+            // (scalar loads, see RT_SPEC_SGEO)
+            double gl[GEO];
+#pragma unroll
+            for (int q = 0; q < GEO; q++) gl[q] = sgeo[i * GEO + q];
+            trace_obj(i, spec_kinds[i], gl, tr);
+#else
+            trace_obj(i, spec_kinds[i], S.geo + (size_t)i * GEO, tr);
+#endif
+          }
         }
 #else
         if constexpr (STREAM) {
@@ -2463,12 +2566,32 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         bd_trays++;
 #endif
         int ssp = 0;
+#if RT_BVH_CONT
+        int nr = 0;  // the node visited next, kept in registers (see RT_BVH_CONT)
+        uint64_t nm = wave_ballot(tr);
+        bool have = true;
+        for (;;) {
+          int r;
+          uint64_t m;
+          if (have) {
+            r = nr;
+            m = nm;
+            have = false;
+          } else {
+            if (ssp == 0) break;
+            ssp--;
+            r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
+            m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+          }
+#else
         bst.push(ssp, lane, 0, wave_ballot(tr));
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
           const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+#endif
           const bool act = tr && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
           bd_tnodes++;
@@ -2552,6 +2675,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const uint64_t m0 = wave_ballot(a0), m1 = wave_ballot(a1);
             // near child popped first: the one most lanes enter first
             const bool c1_first = 2 * __popcll(wave_ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
+#if RT_BVH_CONT
+            bvh_next(bst, ssp, lane, c1_first, ni[0], ni[1], m0, m1, nr, nm, have);
+#else
             if (c1_first) {
               if (m0) bst.push(ssp, lane, ni[0], m0);
               if (m1) bst.push(ssp, lane, ni[1], m1);
@@ -2559,6 +2685,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               if (m1) bst.push(ssp, lane, ni[1], m1);
               if (m0) bst.push(ssp, lane, ni[0], m0);
             }
+#endif
 #endif
           }
         }
@@ -2721,7 +2848,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #endif
     uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind (cones: below)
     // Direction and distance to a light (raytracer.go:378-380).
-    auto light_dir = [&](const double* lt, d3& ldir, double& dist) {
+    auto light_dir = [&](auto lt, d3& ldir, double& dist) {
       if (spec_feat(SF_LDIR) && (int)lt[9] == RT_LIGHT_DIRECTIONAL) {  // extension: light at infinity
         ldir = mk(lt[6], lt[7], lt[8]);
         dist = __builtin_inf();
@@ -2748,7 +2875,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       bool ok_all = true;
 #pragma unroll
       for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-        const double* lt = S.lights + (size_t)li * LGT;
+        const auto lt = LTP(li);
         bool ok;
         ldir_a[li] = norm_len_core(sub(mk(lt[0], lt[1], lt[2]), pw), dist_a[li], ok);
         ok_all = ok_all & ok;
@@ -2756,17 +2883,17 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if (__builtin_expect(!ok_all, 0)) {
 #pragma unroll
         for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-          const double* lt = S.lights + (size_t)li * LGT;
+          const auto lt = LTP(li);
           ldir_a[li] = norm_len_fix(sub(mk(lt[0], lt[1], lt[2]), pw), dist_a[li]);
         }
       }
     } else {
 #pragma unroll
-      for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(S.lights + (size_t)li * LGT, ldir_a[li], dist_a[li]);
+      for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(LTP(li), ldir_a[li], dist_a[li]);
     }
 #else
 #pragma unroll
-    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(S.lights + (size_t)li * LGT, ldir_a[li], dist_a[li]);
+    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(LTP(li), ldir_a[li], dist_a[li]);
 #endif
     PH_MARK(5);
 #if RT_STREAM_SMEM && !RT_CULL && RT_SHADOW_JOINT && !defined(RT_SPEC_NOBJ)
@@ -2892,7 +3019,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #pragma unroll
       for (int i = 0; i < RT_SPEC_NOBJ; i++) {
         const int k = spec_kinds[i];
+#if RT_SPEC_SGEO
+        double gl[GEO];
+#pragma unroll
+        for (int q = 0; q < GEO; q++) gl[q] = sgeo[i * GEO + q];
+        const double* g = gl;
+#else
         const double* g = S.geo + (size_t)i * GEO;
+#endif
         bool tst[RT_SPEC_NLIGHTS];
         bool anyt = false;
         if (k != RT_PLANE) {
@@ -2926,7 +3060,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               sr.d = ldir_a[li];
               double t;
               int f;
-              if (csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist_a[li], false) && t * rlen < dist_a[li]) {
+              if (csg_hit(CSG_ARGS, P.nobj, CSG_G(i, g), sr, t, f, rlen, dist_a[li], false) && t * rlen < dist_a[li]) {
                 jopen[li] = false;
                 jsend[li] = i + 1;
               }
@@ -2958,14 +3092,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #endif
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-      const double* lt = S.lights + (size_t)li * LGT;
+      const auto lt = LTP(li);
       const int lkind = (int)lt[9];  // wave-uniform
       const d3 ldir = ldir_a[li];
       const double dist = dist_a[li];
 #else
 #define RT_JOINT_SMALL 0
     for (int li = 0; li < P.nlights; li++) {
-      const double* lt = S.lights + (size_t)li * LGT;
+      const auto lt = LTP(li);
       const int lkind = (int)lt[9];  // wave-uniform
       d3 ldir;
       double dist;
@@ -3059,7 +3193,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             bool test = CULL_AND(open, i != hit_i);
 #if RT_CULL
             test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
-                                 : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+                                 : CULL_AND(test, may_hit_plane(sof, sdf, stmax, SHP(i)));
             if (!wave_any(test)) return true;
 #endif
             EXDIAG(k, 1, test);
@@ -3079,15 +3213,22 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           if (!wave_any(open)) break;
           const int k = S.kind[i];
 #endif
+#if RT_SPEC_SGEO && defined(RT_SPEC_NOBJ)
+          double gl[GEO];
+#pragma unroll
+          for (int q = 0; q < GEO; q++) gl[q] = sgeo[i * GEO + q];
+          const double* g = gl;
+#else
           const double* g = S.geo + (size_t)i * GEO;
+#endif
           bool test = CULL_AND(open, i != hit_i);
 #if RT_SHADOW_HOISTED
           test = k != RT_PLANE ? may_hit_oc_a(test, cox[i], coy[i], coz[i], cr2[i], sdf, stmax)
-                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, SHP(i)));
           if (!wave_any(test)) continue;
 #elif RT_CULL
           test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
-                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, SHP(i)));
           if (!wave_any(test)) continue;
 #endif
           EXDIAG(k, 1, test);
@@ -3096,7 +3237,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             int f;
             bool h;
             if constexpr (CSG)
-              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist, false)
+              h = k == RT_CSG ? csg_hit(CSG_ARGS, P.nobj, CSG_G(i, g), sr, t, f, rlen, dist, false)
                               : object_hit(k, g, sr, t, f);
             else
               h = object_hit(k, g, sr, t, f);
@@ -3122,7 +3263,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             int f;
             bool h;
             if constexpr (CSG)
-              h = k == RT_CSG ? csg_hit(S.geo, S.kind, S.csg, P.nobj, g, sr, t, f, rlen, dist, false)
+              h = k == RT_CSG ? csg_hit(CSG_ARGS, P.nobj, CSG_G(i, g), sr, t, f, rlen, dist, false)
                               : object_hit(k, g, sr, t, f);
             else
               h = object_hit(k, g, sr, t, f);
@@ -3134,7 +3275,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         auto shadow_obj = [&](int i, int k, const double* g, bool act) {
           bool test = CULL_AND(CULL_AND(act, i != hit_i), i < occ);
           test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
-                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, S.shade + (size_t)i * SHD));
+                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, SHP(i)));
           if (!wave_any(test)) return;
           shadow_exact(i, k, g, test);
         };
@@ -3150,12 +3291,32 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         bd_srays++;
 #endif
         int ssp = 0;
+#if RT_BVH_CONT
+        int nr = 0;
+        uint64_t nm = wave_ballot(hit);
+        bool have = true;
+        for (;;) {
+          int r;
+          uint64_t m;
+          if (have) {
+            r = nr;
+            m = nm;
+            have = false;
+          } else {
+            if (ssp == 0) break;
+            ssp--;
+            r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
+            m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+          }
+#else
         bst.push(ssp, lane, 0, wave_ballot(hit));
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
           const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+#endif
           const bool act = hit && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
           bd_snodes++;
@@ -3224,6 +3385,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             // lower-index subtree popped first: it can prune the other
             const bool c1_first = ni[3] < ni[2];
 #endif
+#if RT_BVH_CONT
+            bvh_next(bst, ssp, lane, c1_first, ni[0], ni[1], m0, m1, nr, nm, have);
+#else
             if (c1_first) {
               if (m0) bst.push(ssp, lane, ni[0], m0);
               if (m1) bst.push(ssp, lane, ni[1], m1);
@@ -3231,6 +3395,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               if (m1) bst.push(ssp, lane, ni[1], m1);
               if (m0) bst.push(ssp, lane, ni[0], m0);
             }
+#endif
 #endif
           }
         }
@@ -3268,7 +3433,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     }
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-      const double* lt = S.lights + (size_t)li * LGT;
+      const auto lt = LTP(li);
       if (open_a[li]) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
         if (spec_feat(SF_LSPOT) && (int)lt[9] == RT_LIGHT_SPOT) {  // extension: cone falloff

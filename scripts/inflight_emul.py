@@ -32,10 +32,12 @@ def main():
     ctxs = []
     for _ in range(max(fs)):
         c = pkg.RenderContext(0, specialize=True)
+        if os.environ.get("INFLIGHT_SHARE", "0") == "1":  # work sharing compiled into the kernel
+            c.set_work_sharing(True)
         c.set_scene(packed)
         ctxs.append(c)
     streams = [torch.cuda.Stream(dev) for _ in ctxs]
-    out = {"config": cfg, "steps": steps}
+    out = {"config": cfg, "steps": steps, "work_sharing": os.environ.get("INFLIGHT_SHARE", "0") == "1"}
 
     def wall_ms(F, rank, world):
         drs = [pkg.dist.DistributedRenderer(ctxs[i], packed, rank, world, dev, mode="interleaved")
