@@ -260,6 +260,7 @@ struct DevScene {
   bool branching = false;  // some material is reflective and transparent, or a surface program may make one
   int leaf_kind_mask = 0;  // bit k: some CSG leaf has kind k
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0, off_arec = 0;
+  double bvh_lo[3] = {0, 0, 0}, bvh_hi[3] = {0, 0, 0};  // padded box of the BVH objects (far_shift)
   int nruns = 0;
 };
 
@@ -283,6 +284,9 @@ bool axis_sphere(const double* m) {
 #define RT_BVH_SAH 1  // binned-SAH splits (median split when degenerate)
 #endif
 // Scenes with at least this many bounded objects use the BVH flavour.
+#ifndef RT_FAR_MIN_OBJ
+#define RT_FAR_MIN_OBJ 1024  // BVH scenes from this many objects keep the far-origin shift when specialised
+#endif
 #ifndef RT_BVH_MIN
 #define RT_BVH_MIN 12
 #endif
@@ -524,10 +528,11 @@ struct SpecKey {
   int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
   int quads = 0;                         // pixel schedule: SCH_SERIAL / SCH_QUADS / SCH_PAIRS (pick_schedule)
   int share = 0;                         // work sharing at the tail (rt_set_work_sharing): -DRT_SHARE=1
+  int far = 1;                           // 0: -DRT_FAR_SHIFT=0 (BVH scenes below RT_FAR_MIN_OBJ objects)
   std::string str() const {
     return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
            std::to_string(kmask) + ":" + std::to_string(feat) + ":" + std::to_string(nlights) + ":" + std::to_string(pow_bits) +
-           ":" + std::to_string(nocull) + ":" + std::to_string(quads) + ":" + std::to_string(share);
+           ":" + std::to_string(nocull) + ":" + std::to_string(quads) + ":" + std::to_string(share) + ":" + std::to_string(far);
   }
 };
 
@@ -855,6 +860,10 @@ bool spec_key(const DevScene& s, SpecKey* k) {
             ((s.light_mask >> RT_LIGHT_SPOT) & 1 ? SF_LSPOT : 0);
   k->nlights = (s.nlights >= 1 && s.nlights <= SPEC_MAX_LIGHTS) ? s.nlights : 0;
   k->pow_bits = s.num_programs ? 7 : s.pow_bits;  // surface programs set exponents at run time
+  // the BVH culls' far-origin shift (rt_render.h far_shift) pays where a
+  // far ray would otherwise sweep many leaves (C5 serial 347 -> 120 ms); a
+  // small BVH only carries its registers (C4 +3 %)
+  k->far = (!s.use_bvh || s.nobj >= RT_FAR_MIN_OBJ) ? 1 : 0;
   return true;
 }
 
@@ -877,6 +886,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   if (sk.nocull) defs.push_back("-DRT_CULL=0");
   if (sk.share) defs.push_back("-DRT_SHARE=1");
   if (sk.quads == SCH_PAIRS) defs.push_back("-DRT_PAIRS=1");
+  if (!sk.far) defs.push_back("-DRT_FAR_SHIFT=0");
   std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
   for (const auto& d : defs) opts.push_back(d.c_str());
   // RT_SPEC_EXTRA_FLAGS: extra compiler options (tuning experiments only);
@@ -1673,6 +1683,22 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     if (!runs.empty()) std::memcpy(acc.data() + s.off_runs, runs.data(), runs.size() * sizeof(int));
     if (!arec.empty()) std::memcpy(acc.data() + s.off_arec, arec.data(), arec.size() * sizeof(double));
     if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
+    if (s.use_bvh && !b.nodes.empty()) {
+      // the root's two child boxes (the padded bounding spheres, rounded
+      // outwards) and a generous pad: every BVH object lies inside
+      const float* nb = b.nodes.data();
+      double ext = 0.0;
+      for (int k = 0; k < 3; k++) {
+        s.bvh_lo[k] = std::min((double)nb[k], (double)nb[6 + k]);
+        s.bvh_hi[k] = std::max((double)nb[3 + k], (double)nb[9 + k]);
+        ext = std::max(ext, s.bvh_hi[k] - s.bvh_lo[k]);
+      }
+      const double pad = 1e-3 * (1.0 + ext);
+      for (int k = 0; k < 3; k++) {
+        s.bvh_lo[k] -= pad;
+        s.bvh_hi[k] += pad;
+      }
+    }
     if (!b.leaf_geo.empty())
       std::memcpy(acc.data() + s.off_bobj, b.leaf_geo.data(), b.leaf_geo.size() * sizeof(double));
     if (!planes.empty()) std::memcpy(acc.data() + s.off_planes, planes.data(), planes.size() * sizeof(int));
@@ -1944,6 +1970,10 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
     P.planes = reinterpret_cast<const int*>(s.accel + s.off_planes);
     P.nplanes = s.nplanes;
     P.bvh_stack_off = stack_off;
+    for (int k = 0; k < 3; k++) {
+      P.bvh_lo[k] = s.bvh_lo[k];
+      P.bvh_hi[k] = s.bvh_hi[k];
+    }
   }
 
   // Launches on a context alternate between two sets of queue heads, each

@@ -238,6 +238,7 @@ struct Params {
   const double* bvh_geo;   // leaf objects in BVH order: geo record, 14 = index, 15 = kind
   const int* planes;       // unbounded objects, ascending index
   int nplanes, bvh_stack_off;
+  double bvh_lo[3], bvh_hi[3];  // padded box around every BVH object (far_shift)
   // Global linear scenes: maximal runs of consecutive objects of one kind,
   // [nruns][4] = first index, count, kind, 0 (brute-force scalar-load loops)
   const int* runs;
@@ -346,8 +347,8 @@ struct RecN {
 typedef RecN<12> Rec12;  // WorldToObject rows (geo records, GEO doubles apart)
 typedef RecN<6> Rec6;    // axis-aligned sphere: m0 m3 m5 m7 m10 m11 (arec, AXIS_REC doubles apart)
 enum { AXIS_REC = 8 };
-template <int N>
-__device__ __forceinline__ RecN<N> ld_rec(cdptr p) {
+template <int N, typename PT>
+__device__ __forceinline__ RecN<N> ld_rec(PT p) {
   RecN<N> r;
 #pragma unroll
   for (int q = 0; q < N; q++) r.m[q] = p[q];
@@ -379,8 +380,8 @@ struct LeafRec {
   bool ax;  // a scale + translation sphere (host: axis_sphere)
 #endif
 };
-__device__ __forceinline__ LeafRec ld_leaf(const double* base, int j) {
-  const cdptr p = (cdptr)base + (size_t)j * 16;
+template <typename PT>
+__device__ __forceinline__ LeafRec ld_leaf_p(PT p) {
   LeafRec L;
   L.R = ld_rec<12>(p);
   const uint64_t b0 = (uint64_t)__double_as_longlong(p[12]), b1 = (uint64_t)__double_as_longlong(p[13]);
@@ -396,6 +397,24 @@ __device__ __forceinline__ LeafRec ld_leaf(const double* base, int j) {
   L.k = (int)(uint32_t)(uint64_t)__double_as_longlong(p[15]);
   return L;
 }
+__device__ __forceinline__ LeafRec ld_leaf(const double* base, int j) {
+  return ld_leaf_p((cdptr)base + (size_t)j * 16);  // wave-uniform j: scalar loads
+}
+// Per-lane BVH traversal (RT_BVH_LANE): the wave-coherent traversal visits the
+// union of its lanes' nodes, which for rays that thread the gaps of a dense
+// lattice (C5's horizon rows) grows to thousands of nodes per pass while each
+// ray alone visits a few hundred. After RT_BVH_LANE_AFTER wave node visits a
+// traversal hands its remaining stack entries to the lanes (each lane takes
+// the entries whose mask holds it, in stack order) and every lane finishes on
+// its own stack in private memory, with vector loads. The closest hit (ties on
+// the lowest index) and the lowest-index occluder do not depend on the visit
+// order, so results and counters are unchanged.
+#ifndef RT_BVH_LANE
+#define RT_BVH_LANE 0
+#endif
+#ifndef RT_BVH_LANE_AFTER
+#define RT_BVH_LANE_AFTER 256
+#endif
 // Index of the next record to prefetch, made to depend on the current record
 // (an empty asm that "reads" it): scalar loads return out of order, so the
 // only wait the compiler can emit is lgkmcnt(0); this places that wait before
@@ -884,6 +903,42 @@ __device__ __forceinline__ void bvh_next(WaveStack& st, int& sp, int lane, bool 
     nr = sr;
     nm = sm;
     have = true;
+  }
+}
+// Rays from far away (a ground-plane hit near the horizon can lie 1e7 units
+// out): the FP32 culls widen every box and sphere by the origin's rounding
+// scale (ray_slack), which then exceeds the scene and turns the BVH into a
+// brute-force sweep over every leaf. For the BVH culls only, such a lane's
+// origin moves (FP64) to just before where the ray enters the box of all BVH
+// objects, o' = o + t0 d, and its bounds become tmax - t0; a lane whose ray
+// misses that box takes no part. Objects lie in the box, so every cull that
+// could pass for o passes for o' (both conservative); the exact tests still
+// use the reference's ray, so hits and counters do not change.
+#ifndef RT_FAR_SHIFT
+#define RT_FAR_SHIFT 1
+#endif
+__device__ __forceinline__ void far_shift(bool& act, const Ray& r, const double* lo, const double* hi, F3& of,
+                                          float& slack, double& t0) {
+  if (!RT_FAR_SHIFT || !wave_any(act && slack > 1e-3f)) return;
+  if (act && slack > 1e-3f) {
+    const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    double tn = 0.0, tf = __builtin_inf();
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      // d = 0: +-inf (inside the slab: no bound; outside: empty); 0/0 = NaN is
+      // ignored by fmin/fmax
+      const double ta = (lo[a] - o[a]) / d[a], tb = (hi[a] - o[a]) / d[a];
+      tn = __builtin_fmax(tn, __builtin_fmin(ta, tb));
+      tf = __builtin_fmin(tf, __builtin_fmax(ta, tb));
+    }
+    if (!(tn <= tf)) {
+      act = false;
+    } else {
+      t0 = tn * (1.0 - 1e-9);
+      const d3 os = add(r.o, scale(r.d, t0));
+      of = f3(os);
+      slack = ray_slack(of);
+    }
   }
 }
 __device__ __forceinline__ F3 f3_rcp(F3 d) {
@@ -1867,6 +1922,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (lane == 0 && n) atomicAdd(&cnt[k * WAVES_PER_WG + wave], (unsigned long long)n);
   };
   WaveStack bst;
+#if RT_BVH_LANE
+  int lst[BVH ? BVH_STACK : 1];  // per-lane BVH stack (private memory; see RT_BVH_LANE)
+#endif
   bst.mask = reinterpret_cast<uint64_t*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
   bst.ref = reinterpret_cast<int*>(smem + P.bvh_stack_off + WAVES_PER_WG * BVH_STACK * 8) + (threadIdx.x >> 6) * BVH_STACK;
 #ifdef RT_PHASE_TIMING
@@ -2558,6 +2616,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           trace_obj(i, S.kind[i], S.geo + (size_t)i * GEO, tr);
         }
         const F3 idf = f3_rcp(df);
+        // far origins: the BVH culls' origin, slack and bounds (see far_shift)
+        F3 bof = of;
+        float bslack = slack;
+        double bt0 = 0.0;
+        bool btr = tr;
+        far_shift(btr, ray, P.bvh_lo, P.bvh_hi, bof, bslack, bt0);
 #if RT_AXIS_LEAF
         // leaves' scale + translation spheres take the diagonal transform (exact, see axis_o)
         const bool rax = wave_all(!tr || (axis_o_ok(ray.o) && axis_d_ok(ray.d)));
@@ -2568,7 +2632,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         int ssp = 0;
 #if RT_BVH_CONT
         int nr = 0;  // the node visited next, kept in registers (see RT_BVH_CONT)
-        uint64_t nm = wave_ballot(tr);
+        uint64_t nm = wave_ballot(btr);
         bool have = true;
         for (;;) {
           int r;
@@ -2585,14 +2649,69 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                 (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
           }
 #else
-        bst.push(ssp, lane, 0, wave_ballot(tr));
+        bst.push(ssp, lane, 0, wave_ballot(btr));
+#if RT_BVH_LANE && !RT_BVH4
+        int nvis = 0;
+#endif
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
           const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+#if RT_BVH_LANE && !RT_BVH4
+          if (++nvis > RT_BVH_LANE_AFTER) {  // per-lane from here (see RT_BVH_LANE)
+            int lsp = 0;
+            bool ovf = false;
+            auto lpush = [&](int x) {
+              if (lsp < BVH_STACK)
+                lst[lsp++] = x;
+              else
+                ovf = true;
+            };
+            for (int e = 0; e <= ssp; e++) {  // (entry ssp: the one just popped)
+              const int re = __builtin_amdgcn_readfirstlane(bst.ref[e]);
+              const uint64_t me = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[e] >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[e]);
+              if (btr && ((me >> lane) & 1)) lpush(re);
+            }
+            ssp = 0;
+            for (;;) {
+              const bool live = lsp > 0;
+              if (!wave_any(live)) break;
+              if (live) {
+                const int rl = lst[--lsp];
+                if (rl & 7) {
+                  const int first = rl >> 3, count = rl & 7;
+                  for (int j = first; j < first + count; j++) {
+                    const LeafRec L = ld_leaf_p(P.bvh_geo + (size_t)j * 16);  // vector loads
+                    const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
+                    if (may_hit_s(true, bof, df, tmax, L.cx, L.cy, L.cz, L.cr, bslack)) trace_exact(L.i, L.k, L.R.m, true);
+                  }
+                } else {
+                  const float* nb = P.bvh_nodes + (size_t)(rl >> 3) * BN;
+                  const int* ni = reinterpret_cast<const int*>(nb + 12);
+                  const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
+                  float t0 = 0.0f, t1 = 0.0f;
+                  const bool a0 = may_hit_box_a(true, bof, idf, bslack, tmax, nb, t0);
+                  const bool a1 = may_hit_box_a(true, bof, idf, bslack, tmax, nb + 6, t1);
+                  if (a0 && a1) {  // nearer child on top
+                    const bool c1n = t1 < t0;
+                    lpush(c1n ? ni[0] : ni[1]);
+                    lpush(c1n ? ni[1] : ni[0]);
+                  } else if (a0) {
+                    lpush(ni[0]);
+                  } else if (a1) {
+                    lpush(ni[1]);
+                  }
+                }
+              }
+            }
+            if (wave_any(ovf) && lane == 0) atomicAdd(P.stats + ST_WATCHDOG, 1ull);
+            break;
+          }
 #endif
-          const bool act = tr && ((m >> lane) & 1);
+#endif
+          const bool act = btr && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
           bd_tnodes++;
 #ifdef RT_COST_MAP
@@ -2607,8 +2726,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             for (int j = first; j < first + count; j++) {
               // the leaf's record through scalar loads (wave-uniform index)
               const LeafRec L = ld_leaf(P.bvh_geo, j);
-              const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
-              const bool test = may_hit_s(act, of, df, tmax, L.cx, L.cy, L.cz, L.cr, slack);
+              const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
+              const bool test = may_hit_s(act, bof, df, tmax, L.cx, L.cy, L.cz, L.cr, bslack);
               if (!wave_any(test)) continue;
 #if RT_AXIS_LEAF
               if (spec_kind(RT_SPHERE) && L.k == RT_SPHERE && L.ax && rax) {
@@ -2636,7 +2755,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #if RT_BVH4
             const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN4;  // scalar loads
             const ciptr ni = (ciptr)(nb + 24);
-            const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+            const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
             const int fl = __builtin_ctzll(m);  // the node's first lane: its entry distances order the children
             uint64_t cm[4];
             uint32_t ck[4];
@@ -2645,7 +2764,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             for (int c = 0; c < 4; c++) {
               cr[c] = ni[c];
               float tn = 0.0f;
-              const bool a = may_hit_box6_a(act, of, idf, slack, tmax, nb[c], nb[4 + c], nb[8 + c], nb[12 + c],
+              const bool a = may_hit_box6_a(act, bof, idf, bslack, tmax, nb[c], nb[4 + c], nb[8 + c], nb[12 + c],
                                             nb[16 + c], nb[20 + c], tn);
               cm[c] = cr[c] >= 0 ? wave_ballot(a) : 0ull;
               ck[c] = f_order_key(__builtin_amdgcn_readlane(__float_as_int(tn), fl));
@@ -2668,10 +2787,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #else
             const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN;  // scalar loads
             const ciptr ni = (ciptr)(nb + 12);
-            const float tmax = found ? (float)best_t * 1.0001f + 1e-4f : 3.0e38f;
+            const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
             float t0 = 0.0f, t1 = 0.0f;  // (set by may_hit_box when it returns true)
-            const bool a0 = may_hit_box_a(act, of, idf, slack, tmax, nb, t0);
-            const bool a1 = may_hit_box_a(act, of, idf, slack, tmax, nb + 6, t1);
+            const bool a0 = may_hit_box_a(act, bof, idf, bslack, tmax, nb, t0);
+            const bool a1 = may_hit_box_a(act, bof, idf, bslack, tmax, nb + 6, t1);
             const uint64_t m0 = wave_ballot(a0), m1 = wave_ballot(a1);
             // near child popped first: the one most lanes enter first
             const bool c1_first = 2 * __popcll(wave_ballot(a0 && a1 && t1 < t0)) > __popcll(m0 & m1);
@@ -3284,6 +3403,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           shadow_obj(i, S.kind[i], S.geo + (size_t)i * GEO, hit);
         }
         const F3 sidf = f3_rcp(sdf);
+        // far origins: the BVH culls' origin, slack and bound (see far_shift)
+        F3 sbof = sof;
+        float sbslack = sslack;
+        double sbt0 = 0.0;
+        bool sact = hit;
+        far_shift(sact, sr, P.bvh_lo, P.bvh_hi, sbof, sbslack, sbt0);
+        const float sbtmax = sbt0 == 0.0 ? stmax : (float)(dist / rlen - sbt0) * 1.0001f + 1e-4f;
 #if RT_AXIS_LEAF
         const bool sax = wave_all(!hit || (axis_o_ok(sr.o) && axis_d_ok(sr.d)));
 #endif
@@ -3293,7 +3419,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         int ssp = 0;
 #if RT_BVH_CONT
         int nr = 0;
-        uint64_t nm = wave_ballot(hit);
+        uint64_t nm = wave_ballot(sact);
         bool have = true;
         for (;;) {
           int r;
@@ -3310,14 +3436,68 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                 (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
           }
 #else
-        bst.push(ssp, lane, 0, wave_ballot(hit));
+        bst.push(ssp, lane, 0, wave_ballot(sact));
+#if RT_BVH_LANE && !RT_BVH4
+        int nvis = 0;
+#endif
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
           const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
+#if RT_BVH_LANE && !RT_BVH4
+          if (++nvis > RT_BVH_LANE_AFTER) {  // per-lane from here (see RT_BVH_LANE)
+            int lsp = 0;
+            bool ovf = false;
+            auto lpush = [&](int x) {
+              if (lsp < BVH_STACK)
+                lst[lsp++] = x;
+              else
+                ovf = true;
+            };
+            for (int e = 0; e <= ssp; e++) {
+              const int re = __builtin_amdgcn_readfirstlane(bst.ref[e]);
+              const uint64_t me = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[e] >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[e]);
+              if (sact && ((me >> lane) & 1)) lpush(re);
+            }
+            ssp = 0;
+            for (;;) {
+              const bool live = lsp > 0;
+              if (!wave_any(live)) break;
+              if (live) {
+                const int rl = lst[--lsp];
+                if (rl & 7) {
+                  const int first = rl >> 3, count = rl & 7;
+                  for (int j = first; j < first + count; j++) {
+                    const LeafRec L = ld_leaf_p(P.bvh_geo + (size_t)j * 16);  // vector loads
+                    if (may_hit_s(L.i != hit_i && L.i < occ, sbof, sdf, sbtmax, L.cx, L.cy, L.cz, L.cr, sbslack))
+                      shadow_exact(L.i, L.k, L.R.m, true);
+                  }
+                } else {
+                  const float* nb = P.bvh_nodes + (size_t)(rl >> 3) * BN;
+                  const int* ni = reinterpret_cast<const int*>(nb + 12);
+                  float t0 = 0.0f, t1 = 0.0f;
+                  const bool a0 = may_hit_box_a(ni[2] < occ, sbof, sidf, sbslack, sbtmax, nb, t0);
+                  const bool a1 = may_hit_box_a(ni[3] < occ, sbof, sidf, sbslack, sbtmax, nb + 6, t1);
+                  if (a0 && a1) {  // lower-index subtree on top
+                    const bool c1f = ni[3] < ni[2];
+                    lpush(c1f ? ni[0] : ni[1]);
+                    lpush(c1f ? ni[1] : ni[0]);
+                  } else if (a0) {
+                    lpush(ni[0]);
+                  } else if (a1) {
+                    lpush(ni[1]);
+                  }
+                }
+              }
+            }
+            if (wave_any(ovf) && lane == 0) atomicAdd(P.stats + ST_WATCHDOG, 1ull);
+            break;
+          }
 #endif
-          const bool act = hit && ((m >> lane) & 1);
+#endif
+          const bool act = sact && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
           bd_snodes++;
 #ifdef RT_COST_MAP
@@ -3331,8 +3511,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const int first = r >> 3, count = r & 7;
             for (int j = first; j < first + count; j++) {
               const LeafRec L = ld_leaf(P.bvh_geo, j);  // scalar loads
-              const bool test = may_hit_s(CULL_AND(CULL_AND(act, L.i != hit_i), L.i < occ), sof, sdf, stmax, L.cx,
-                                          L.cy, L.cz, L.cr, sslack);
+              const bool test = may_hit_s(CULL_AND(CULL_AND(act, L.i != hit_i), L.i < occ), sbof, sdf, sbtmax, L.cx,
+                                          L.cy, L.cz, L.cr, sbslack);
               if (!wave_any(test)) continue;
 #if RT_AXIS_LEAF
               if (spec_kind(RT_SPHERE) && L.k == RT_SPHERE && L.ax && sax) {
@@ -3361,7 +3541,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #pragma unroll
             for (int c = 0; c < 4; c++) {
               float tn = 0.0f;
-              const bool a = may_hit_box6_a(CULL_AND(act, ni[4 + c] < occ), sof, sidf, sslack, stmax, nb[c],
+              const bool a = may_hit_box6_a(CULL_AND(act, ni[4 + c] < occ), sbof, sidf, sbslack, sbtmax, nb[c],
                                             nb[4 + c], nb[8 + c], nb[12 + c], nb[16 + c], nb[20 + c], tn);
               cm[c] = ni[c] >= 0 ? wave_ballot(a) : 0ull;
             }
@@ -3372,8 +3552,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN;  // scalar loads
             const ciptr ni = (ciptr)(nb + 12);
             float t0 = 0.0f, t1 = 0.0f;
-            const bool a0 = may_hit_box_a(CULL_AND(act, ni[2] < occ), sof, sidf, sslack, stmax, nb, t0);
-            const bool a1 = may_hit_box_a(CULL_AND(act, ni[3] < occ), sof, sidf, sslack, stmax, nb + 6, t1);
+            const bool a0 = may_hit_box_a(CULL_AND(act, ni[2] < occ), sbof, sidf, sbslack, sbtmax, nb, t0);
+            const bool a1 = may_hit_box_a(CULL_AND(act, ni[3] < occ), sbof, sidf, sbslack, sbtmax, nb + 6, t1);
             const uint64_t m0 = wave_ballot(a0), m1 = wave_ballot(a1);
 #ifndef RT_SHADOW_NEAR_FIRST
 #define RT_SHADOW_NEAR_FIRST 0  // measured: near-first shadow order is slower (C5 695 -> 822 ms)

@@ -29,6 +29,10 @@ def main():
     print("max at x=%d y=%d" % (x, y))
     # 8x8 tile sums (one wave chunk each)
     t = cost[:h // 8 * 8, :w // 8 * 8].reshape(h // 8, 8, w // 8, 8).sum(axis=(1, 3))
+    top = np.argsort(cost.ravel())[::-1][:int(os.environ.get("COST_TOP", "20"))]
+    for k in top:
+        yy, xx = divmod(int(k), w)
+        print("  pixel x=%d y=%d cost %d" % (xx, yy, cost[yy, xx]))
     ts = np.sort(t.ravel())
     print("tile sums: mean %.0f max %d top5 %s" % (ts.mean(), ts[-1], ts[-5:].tolist()))
     ty, tx = np.unravel_index(np.argmax(t), t.shape)

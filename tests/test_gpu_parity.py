@@ -514,6 +514,20 @@ def test_specialised_kind_mask_scenes_match_oracle(spec_ctx, seed, n, ext):
     assert st.as_dict() == ost.as_dict()
 
 
+@pytest.mark.parametrize("specialise", [False, True])
+def test_c5_horizon_rows_match_oracle(ctx, spec_ctx, specialise):
+    # The rows around the horizon: rays that graze the ground plane hit it up
+    # to ~1e5 units out, so their shadow and reflection rays start far away
+    # and take the BVH culls' far-origin shift (rt_render.h far_shift).
+    packed = rt.scene.convert(rt.configs.c5(width=960, height=540))
+    c = spec_ctx if specialise else ctx
+    img, st = render(c, packed, 266, 274)
+    assert c.specialized()[0] == specialise
+    ref, ost = oracle_bind.render_rows(packed, 266, 274)
+    assert_same(img, ref, "c5 horizon rows")
+    assert st.as_dict() == ost.as_dict()
+
+
 def test_specialised_c5_rows_match_oracle(spec_ctx):
     packed = rt.scene.convert(rt.configs.c5(width=96, height=60))
     spec_ctx.set_scene(packed)
