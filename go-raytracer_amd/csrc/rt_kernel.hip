@@ -1684,15 +1684,19 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     if (!arec.empty()) std::memcpy(acc.data() + s.off_arec, arec.data(), arec.size() * sizeof(double));
     if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
     if (s.use_bvh && !b.nodes.empty()) {
-      // the root's two child boxes (the padded bounding spheres, rounded
-      // outwards) and a generous pad: every BVH object lies inside
-      const float* nb = b.nodes.data();
+      // the box of the BVH objects' padded bounding spheres, and a generous
+      // pad: every BVH object lies inside
       double ext = 0.0;
       for (int k = 0; k < 3; k++) {
-        s.bvh_lo[k] = std::min((double)nb[k], (double)nb[6 + k]);
-        s.bvh_hi[k] = std::max((double)nb[3 + k], (double)nb[9 + k]);
-        ext = std::max(ext, s.bvh_hi[k] - s.bvh_lo[k]);
+        s.bvh_lo[k] = 1e300;
+        s.bvh_hi[k] = -1e300;
       }
+      for (int i : b.ord)
+        for (int k = 0; k < 3; k++) {
+          s.bvh_lo[k] = std::min(s.bvh_lo[k], bcen[(size_t)i * 3 + k] - brad[i]);
+          s.bvh_hi[k] = std::max(s.bvh_hi[k], bcen[(size_t)i * 3 + k] + brad[i]);
+        }
+      for (int k = 0; k < 3; k++) ext = std::max(ext, s.bvh_hi[k] - s.bvh_lo[k]);
       const double pad = 1e-3 * (1.0 + ext);
       for (int k = 0; k < 3; k++) {
         s.bvh_lo[k] -= pad;
