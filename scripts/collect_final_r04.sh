@@ -23,3 +23,14 @@ cp $SRC/sweep/*.json $DST/sweep/ 2>/dev/null || true
 cp $SRC/strong/*.json $DST/strong/ 2>/dev/null || true
 cp $SRC/pytest_gpu.log $DST/ 2>/dev/null || true
 echo collected into $DST
+# brute-force C5 band (part C: scripts/gpu_brute_pmc.sh r4final)
+B=gpurun_out/brute_r4final
+if [ -d $B ]; then
+  mkdir -p $DST/brute
+  for p in p1 p2; do cp $B/$p/${p}_counter_collection.csv profiles/r04/pmc_csv/c5bf_${p}_counter_collection.csv; done
+  python3 scripts/pmc_roofline.py "profiles/r04/pmc_csv/c5bf_p[12]_*.csv" profiles/pmc_c5_bf_rows2048-2304.json rt_render > /dev/null
+  cp $B/bench.json $B/summary.txt $B/kernel_stats.csv $DST/brute/ 2>/dev/null || true
+  cp $B/phase.err $DST/brute/ 2>/dev/null || true
+fi
+cp $SRC/strong/*.err $DST/strong/ 2>/dev/null || true
+cp $SRC/pmc_all.log $DST/ 2>/dev/null || true

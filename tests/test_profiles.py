@@ -46,14 +46,14 @@ def test_bench_reads_the_committed_summary():
 
 
 def test_committed_bench_line_keeps_the_contract():
-    """The committed round bench line (profiles/r03/final3/bench_c3.json) has the
+    """The committed round bench line (profiles/r04/final/bench_c3.json) has the
     driver's fields, and its derived numbers agree with each other: value =
     rays per step / ms per step, frac = achieved / peak, and the GPU span per
     frame from the rocprofv3 kernel trace of the same command
     (scripts/trace_span.py; frames in flight overlap, so the span, not a
     dispatch's duration, is the kernel time) is within 5 % of the in-bench
     kernel time."""
-    d = json.load(open(os.path.join(ROOT, "profiles", "r03", "final3", "bench_c3.json")))
+    d = json.load(open(os.path.join(ROOT, "profiles", "r04", "final", "bench_c3.json")))
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
@@ -67,9 +67,9 @@ def test_committed_bench_line_keeps_the_contract():
     assert r["kernel_ms"] <= d["ms_per_step"] * 1.001
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
-    t = json.load(open(os.path.join(ROOT, "profiles", "r03", "final3", "trace_span_c3.json")))
+    t = json.load(open(os.path.join(ROOT, "profiles", "r04", "final", "trace_span_c3.json")))
     assert t["dispatches"] == 30
-    prof = json.load(open(os.path.join(ROOT, "profiles", "r03", "final3", "rocprof_bench.json")))
+    prof = json.load(open(os.path.join(ROOT, "profiles", "r04", "final", "rocprof_bench.json")))
     assert t["span_ms_per_frame"] == pytest.approx(prof["roofline"]["kernel_ms"], rel=0.05)
     assert t["span_ms_per_frame"] == pytest.approx(r["kernel_ms"], rel=0.05)
 
