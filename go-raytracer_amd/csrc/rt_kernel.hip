@@ -287,6 +287,9 @@ bool axis_sphere(const double* m) {
 #ifndef RT_FAR_MIN_OBJ
 #define RT_FAR_MIN_OBJ 1024  // BVH scenes from this many objects keep the far-origin shift when specialised
 #endif
+#ifndef RT_BVH_LEAF
+#define RT_BVH_LEAF 4  // objects per BVH leaf (<= 7: the leaf ref holds the count in 3 bits)
+#endif
 #ifndef RT_BVH_MIN
 #define RT_BVH_MIN 12
 #endif
@@ -340,7 +343,7 @@ struct BvhBuild {
       out.box[k] = f_down(bl[k]);
       out.box[3 + k] = f_up(bh[k]);
     }
-    if (hi - lo <= 4) {
+    if (hi - lo <= RT_BVH_LEAF) {
       std::sort(ord.begin() + lo, ord.begin() + hi);
       const int first = (int)(leaf_geo.size() / GEO);
       for (int j = lo; j < hi; j++) {
