@@ -38,6 +38,10 @@ CASES = {
 # seeds) of the full 7680-wide, 4320-row frame, 100 000 spheres, depth 8.
 FULL = {
     "c5_7680x4320_rows2140-2160": ("c5", 7680, 4320, (2140, 2160)),
+    # the horizon rows: rays that meet the ground plane up to ~1e7 units out,
+    # whose shadow and reflection rays take the BVH culls' far-origin shift
+    # (rt_render.h far_shift)
+    "c5_7680x4320_rows2156-2164": ("c5", 7680, 4320, (2156, 2164)),
 }
 
 
@@ -70,6 +74,16 @@ def write(cases, meta_name, threads=8):
 def main():
     if "--full" in sys.argv:  # minutes: the 100k-sphere brute-force strip
         write(FULL, "counters_full.json", threads=os.cpu_count() or 8)
+    elif "--full-only" in sys.argv:  # --full-only NAME: add one full-size strip
+        name = sys.argv[sys.argv.index("--full-only") + 1]
+        path = os.path.join(HERE, "synthetic", "counters_full.json")
+        meta = json.load(open(path)) if os.path.exists(path) else {}
+        write({name: FULL[name]}, "counters_full.json.new", threads=os.cpu_count() or 8)
+        new = os.path.join(HERE, "synthetic", "counters_full.json.new")
+        meta.update(json.load(open(new)))
+        os.remove(new)
+        with open(path, "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
     else:
         write(CASES, "counters.json")
 
