@@ -449,7 +449,8 @@ def main():
                 "issue_util": round(ex["issue_util"], 4),
                 "lane_util": round(ex["lane_util"], 4),
                 "pmc_source": exsrc})
-        tb, src, tsrc = pmc_traffic(args.config)
+        # (the traffic summary of the accelerated search: not quoted for --accel none)
+        tb, src, tsrc = pmc_traffic(args.config) if args.accel != "none" else (None, None, None)
         if tb is not None and tsrc != pkg.render.kernel_source_id():
             line["roofline"]["traffic_stale"] = src  # another kernel build's counters
             tb = None
