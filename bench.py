@@ -79,7 +79,74 @@ def parse():
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
+    p.add_argument("--launch-selftest", action="store_true",
+                   help="CPU test of the N-rank launch and telemetry path: gloo ranks, synthetic "
+                        "per-rank times, no device (tests/test_bench_launch.py)")
     return p.parse_args()
+
+
+def spawn_ranks(n):
+    """`python3 bench.py --gpus N` without a launcher: start the N rank
+    processes here, before anything touches a GPU (one process per GPU,
+    LOCAL_RANK = RANK, rendezvous on 127.0.0.1), wait for them, and return the
+    worst exit status. A rank that fails stops the others. Rank 0 prints the
+    JSON line."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:  # one rank failed: the collectives of the others would hang
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def telemetry(rank_rows):
+    """The N>1 line's per-rank fields from rank_table rows [render span per
+    step (GPU ms), gather cost per frame (ms, -1 = none), wall time (s)]."""
+    per = [{"rank": r, "render_span_ms": round(v[0], 4),
+            "gather_ms": None if v[1] < 0 else round(v[1], 4),
+            "wall_ms_per_step": round(v[2], 4)} for r, v in enumerate(rank_rows)]
+    slow = max(range(len(per)), key=lambda r: per[r]["render_span_ms"])
+    g = [p["gather_ms"] for p in per if p["gather_ms"] is not None]
+    return {"per_rank_ms": per, "slowest_rank": slow,
+            "gather_ms": {"mean": round(sum(g) / len(g), 4), "max": round(max(g), 4)} if g else None}
+
+
+def launch_selftest(args):
+    """Each rank of a gloo world reports synthetic times through the same
+    rank_table / telemetry path the GPU bench uses; rank 0 prints one line."""
+    import torch.distributed as dist
+    pkg = load_package()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    rows = pkg.dist.rank_table([1.0 + rank, 0.25 * (rank + 1) if world > 1 else -1.0, 2.0 + rank])
+    mx, sm = pkg.dist.reduce_max_sum([2.0 + rank, 10.0])
+    if rank == 0:
+        line = {"metric": METRIC, "n_gpus": world, "selftest": True, "max_wall": mx[0], "sum_rays": sm[1]}
+        line.update(telemetry(rows))
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def pmc_traffic(config):
@@ -240,63 +307,54 @@ def side_config(pkg, name, dev, specialize, inflight, streams=None, steps=10, wa
 def render_api_leg(pkg, packed, reps=30, budget_s=20.0):
     """The reference's own seam, timed: rt_render (include/rt_abi.h), the
     synchronous replacement of func Render(*Scene) image.Image
-    (raytracer.go:589-682, hooked at evaluator.go:48): every call converts and
-    uploads the scene (rt_set_scene), renders one frame on the library's cached
-    context and copies the RGBA8 image into pageable host memory (numpy), like
-    Go's image.RGBA. Its context specialises the kernel (rt_set_specialize; the
-    first call with a new scene shape pays the hipRTC compile unless this
-    process already compiled that shape). Reported: the first call in the
-    process (context creation included), the median of the last five of `reps`
-    calls, and one warm call split into its parts through a RenderContext
-    (scene setup, kernel, D2H)."""
+    (raytracer.go:589-682, hooked at evaluator.go:48): every call compares the
+    scene with the last one (converting and uploading it when it changed),
+    renders one frame and copies the RGBA8 image into pageable host memory
+    (numpy), like Go's image.RGBA. Reported: the first call in the process
+    (context creation, scene conversion, hipRTC compile unless this process
+    already compiled that shape, tile-cost estimate), the median of the last
+    five of `reps` calls, and that median call's parts as the library measured
+    them on the same call (rt_render_last_timing: one host timeline, so
+    setup + render_wait + copy_tail = total)."""
     import ctypes
     import numpy as np
-    import torch
     lib = pkg.render.load_library()
     out = np.empty((packed.height, packed.width, 4), np.uint8)
     st = pkg.abi.rt_stats()
-    times = []
+    calls = []
     t_end = time.perf_counter() + budget_s
     for k in range(reps):
         t0 = time.perf_counter()
         rc = lib.rt_render(packed.ref(), out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
-        times.append((time.perf_counter() - t0) * 1e3)
+        wall = (time.perf_counter() - t0) * 1e3
         if rc != 0:
             raise RuntimeError("rt_render failed: %s" % lib.rt_last_error().decode())
+        tm = pkg.abi.rt_render_timing()
+        lib.rt_render_last_timing(ctypes.byref(tm))
+        calls.append((wall, tm.as_dict()))
         if k >= 5 and time.perf_counter() > t_end:
             break
-    last = sorted(times[-5:])
-    # one warm call's parts, on a RenderContext with the same specialisation
-    ctx = pkg.RenderContext(torch.cuda.current_device(), specialize=True)
-    try:
-        for _ in range(3):
-            t0 = time.perf_counter()
-            ctx.set_scene(packed)
-            t_set = (time.perf_counter() - t0) * 1e3
-            ctx.read_stats(reset=True)
-            dev = torch.empty((packed.height, packed.width, 4), dtype=torch.uint8, device=torch.cuda.current_device())
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            ctx.render_rows_async(0, packed.height, dev)
-            torch.cuda.synchronize()
-            t_kern = (time.perf_counter() - t0) * 1e3
-            t0 = time.perf_counter()
-            host = dev.cpu().numpy()
-            t_d2h = (time.perf_counter() - t0) * 1e3
-        spec = bool(ctx.specialized()[0])
-    finally:
-        ctx.close()
-    assert host.shape == out.shape
-    return {"what": "rt_render(scene, host RGBA8, stats): scene conversion + upload + one frame + D2H copy, "
-                    "synchronous (the Render() seam, raytracer.go:589); not part of `value`",
-            "calls": len(times), "first_call_ms": round(times[0], 3), "steady_ms": round(last[len(last) // 2], 3),
-            "parts_ms": {"set_scene": round(t_set, 3), "render_wall": round(t_kern, 3), "d2h_pageable": round(t_d2h, 3),
-                         "kernel": "specialised" if spec else "generic"},
+    last = sorted(calls[-5:], key=lambda c: c[0])
+    wall, parts = last[len(last) // 2]
+    return {"what": "rt_render(scene, host RGBA8, stats): scene compare (+ conversion and upload when it "
+                    "changed) + one frame + copy into pageable host memory, synchronous (the Render() seam, "
+                    "raytracer.go:589); not part of `value`",
+            "calls": len(calls), "first_call_ms": round(calls[0][0], 3), "first_call_parts": calls[0][1],
+            "steady_ms": round(wall, 3),
+            "parts_ms": parts,
+            "parts_def": "library timeline of the median steady call: setup_ms + render_wait_ms + copy_tail_ms "
+                         "= total_ms (wall from Python: steady_ms); gpu_ms = GPU span of its bands",
             "rays_per_call": int(st.primary_rays + st.secondary_rays + st.shadow_rays)}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher (torchrun) set the ranks up: start them here, before any
+        # GPU call in this process
+        sys.exit(spawn_ranks(args.gpus))
+    if args.launch_selftest:
+        return launch_selftest(args)
     pkg = load_package()
     import torch
     import torch.distributed as dist
@@ -350,6 +408,7 @@ def main():
     dr.flush()
     torch.cuda.synchronize()
     dr.read_stats(reset=True)
+    dr.gather_ms()  # (the warm-up gathers are not the timed ones)
 
     # Kernel time: torch events on the launch streams around each render launch
     # inside the timed region, read after it (no host sync per step).
@@ -375,6 +434,9 @@ def main():
     # duration when launches do not overlap, i.e. --inflight 1)
     kavg = span_ms
     lavg = sum(launch_ms) / len(launch_ms) if launch_ms else 0.0
+    gms = dr.gather_ms()
+    rank_rows = pkg.dist.rank_table([span_ms, -1.0 if gms is None else gms, elapsed / args.steps * 1e3],
+                                    device=dev)
     mx, sm = pkg.dist.reduce_max_sum([elapsed, rays_local], device=dev)
     elapsed, rays_total = mx[0], sm[1]
 
@@ -431,6 +493,11 @@ def main():
                          "traffic": None, "traffic_source": None},
             "cpu_baseline": None,
         }
+        if world > 1:
+            # per rank: GPU render span per step, the pipelined gather's cost
+            # per frame (render end -> collective complete, the wait for the
+            # slowest rank included), wall per step
+            line.update(telemetry(rank_rows))
         # What the kernel executes (PMC) next to the reference-algorithmic frac
         key = args.config + ("_bf" if args.accel == "none" else "") + \
             ("_rows%d-%d" % band if band else "")

@@ -5,7 +5,7 @@ sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
-RT_ABI_VERSION = 4  # include/rt_abi.h
+RT_ABI_VERSION = 5  # include/rt_abi.h
 RT_EXP_AMD64_FMA, RT_EXP_AMD64, RT_EXP_PORTABLE = 0, 1, 2  # rt_scene.exp_mode
 
 RT_OK = 0
@@ -133,6 +133,26 @@ class rt_stats(C.Structure):
 
     def total_rays(self):
         return int(self.primary_rays) + int(self.secondary_rays) + int(self.shadow_rays)
+
+
+class rt_render_timing(C.Structure):
+    """Parts of the calling thread's last rt_render call (ABI 5), one host
+    timeline: setup + render_wait + copy_tail = total."""
+    _fields_ = [
+        ("total_ms", C.c_double),
+        ("setup_ms", C.c_double),
+        ("render_wait_ms", C.c_double),
+        ("copy_tail_ms", C.c_double),
+        ("gpu_ms", C.c_double),
+        ("bands", C.c_int32),
+        ("scene_reused", C.c_int32),
+        ("specialized", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+    def as_dict(self):
+        return {k: (round(getattr(self, k), 4) if isinstance(getattr(self, k), float) else int(getattr(self, k)))
+                for k, _ in self._fields_ if k != "reserved"}
 
 
 class PackedScene:

@@ -463,56 +463,6 @@ struct BvhBuild {
     out.ref = node << 3;
     return out;
   }
-
-  // 4-wide BVH (rt_render.h RT_BVH4): node `ref` of the binary tree collapsed
-  // one level -- its children are its binary children's children, or the
-  // binary child itself when that is a leaf -- into nodes4 ([m][BN4]: boxes
-  // SoA, refs, smallest indices; children in ascending smallest index, empty
-  // slots ref -1). Leaf refs are unchanged. Returns the new ref; depth4 and
-  // stack4 (most stack entries a traversal can hold) follow the tree.
-  std::vector<float> nodes4;
-  int depth4 = 0, stack4 = 0;
-  int collapse(int ref, int depth, int pending) {
-    if (ref & 7) return ref;
-    depth4 = std::max(depth4, depth);
-    struct Ch {
-      const float* box;
-      int ref, mn;
-    };
-    Ch ch[4];
-    int n = 0;
-    const float* nb = &nodes[(size_t)(ref >> 3) * BN];
-    const int* ni = reinterpret_cast<const int*>(nb + 12);
-    for (int s = 0; s < 2; s++) {
-      if (ni[s] & 7) {
-        ch[n++] = {nb + 6 * s, ni[s], ni[2 + s]};
-      } else {
-        const float* cb = &nodes[(size_t)(ni[s] >> 3) * BN];
-        const int* ci = reinterpret_cast<const int*>(cb + 12);
-        for (int t = 0; t < 2; t++) ch[n++] = {cb + 6 * t, ci[t], ci[2 + t]};
-      }
-    }
-    std::sort(ch, ch + n, [](const Ch& a, const Ch& b) { return a.mn < b.mn; });
-    const int m = (int)(nodes4.size() / BN4);
-    nodes4.resize(nodes4.size() + BN4, 0.0f);
-    // a traversal here holds the entries pending above plus up to n pushed
-    stack4 = std::max(stack4, pending + n);
-    int cref[4] = {-1, -1, -1, -1}, cmn[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
-    float cbox[4][6] = {};
-    for (int c = 0; c < n; c++) {
-      cref[c] = collapse(ch[c].ref, depth + 1, pending + n - 1);
-      cmn[c] = ch[c].mn;
-      for (int k = 0; k < 6; k++) cbox[c][k] = ch[c].box[k];
-    }
-    float* q = &nodes4[(size_t)m * BN4];
-    int* qi = reinterpret_cast<int*>(q + 24);
-    for (int c = 0; c < 4; c++) {
-      for (int k = 0; k < 6; k++) q[4 * k + c] = cbox[c][k];
-      qi[c] = cref[c];
-      qi[4 + c] = cmn[c];
-    }
-    return m << 3;
-  }
 };
 
 int align16(int v) { return (v + 15) & ~15; }
@@ -1459,6 +1409,8 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
                            : std::numeric_limits<float>::infinity()};
         int w[6];
         std::memcpy(w, gf, sizeof gf);
+        // leaf numbers as bytes, 0xff = end of list (csg_hit): leaf numbers must stay below 255
+        static_assert(RT_CSG_MAX_LEAVES < 255, "CSG leaf groups pack leaf numbers in bytes (0xff ends a list)");
         uint32_t lb[2] = {0xffffffffu, 0xffffffffu};
         for (size_t q = 0; q < gv.size(); q++) {
           lb[q >> 2] &= ~(0xffu << (8 * (q & 3)));
@@ -1639,13 +1591,6 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       b.ord = bounded;
       b.build(0, (int)bounded.size(), 0);  // root: node 0 (> 4 objects)
       s.use_bvh = b.max_depth + 2 < BVH_STACK;
-#if RT_BVH4
-      if (s.use_bvh) {
-        b.collapse(0, 0, 0);  // root: node 0 of nodes4
-        b.nodes.swap(b.nodes4);
-        s.use_bvh = b.stack4 + 2 < BVH_STACK;
-      }
-#endif
     }
     if (!s.use_bvh) {
       b.nodes.clear();
@@ -1715,7 +1660,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       return rc;
     }
     s.nplanes = (int)planes.size();
-    s.nnodes = (int)(b.nodes.size() / (RT_BVH4 ? BN4 : BN));
+    s.nnodes = (int)(b.nodes.size() / BN);
   }
   // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
   int frames = std::max(1, s.depth - 1);
@@ -2267,57 +2212,7 @@ int rt_debug_run_surface(rt_context* c, int program, int n, const long long* fac
   return rc;
 }
 
-int rt_render(const rt_scene* scene, uint8_t* rgba_out, rt_stats* stats) {
-  if (!scene || !rgba_out) return fail(RT_E_INVALID, "rt_render: NULL argument");
-  // one context and one device frame buffer per device, kept between calls
-  // (the reference's Render allocates its image per call, raytracer.go:590)
-  struct Slot {
-    rt_context* c = nullptr;
-    void* buf = nullptr;
-    size_t bytes = 0;
-  };
-  static std::mutex mu;
-  static std::vector<Slot> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if ((int)cache.size() <= dev) cache.resize(dev + 1);
-  Slot& sl = cache[dev];
-  if (!sl.c) {
-    int rc = rt_create(dev, &sl.c);
-    if (rc != RT_OK) return rc;
-    // scene specialisation (hipRTC, cached per process by scene shape): the
-    // first call with a new shape pays the compile; RT_RENDER_SPECIALIZE=0 keeps
-    // the generic kernel (hipRTC runs in its own link-map namespace with its own
-    // libc, so it is only ever called on the caller's thread)
-    const char* e = getenv("RT_RENDER_SPECIALIZE");
-    if (!e || atoi(e) != 0) {
-      rc = rt_set_specialize(sl.c, 1);
-      if (rc != RT_OK) return rc;
-    }
-  }
-  rt_context* c = sl.c;
-  if (scene->width <= 1 || scene->height <= 1) return fail(RT_E_INVALID, "rt_set_scene: width/height must be > 1");
-  const size_t bytes = (size_t)scene->width * scene->height * 4;
-  if (bytes > sl.bytes) {
-    (void)hipFree(sl.buf);
-    sl.buf = nullptr;
-    sl.bytes = 0;
-    DeviceGuard guard(dev);
-    if (hipMalloc(&sl.buf, bytes) != hipSuccess) return fail(RT_E_NOMEM, "rt_render: frame buffer");
-    sl.bytes = bytes;
-  }
-  int rc = rt_set_scene(c, scene);
-  if (rc != RT_OK) return rc;
-  rt_stats tmp;
-  rc = rt_read_stats(c, nullptr, 1, &tmp);
-  if (rc == RT_OK) rc = rt_render_rows_async(c, 0, scene->height, sl.buf, nullptr);
-  if (rc == RT_OK && hipMemcpy(rgba_out, sl.buf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
-    rc = fail(RT_E_DEVICE, "rt_render: copy back failed");
-  if (rc == RT_OK && stats) rc = rt_read_stats(c, nullptr, 1, stats);
-  return rc;
-}
-
 }  // extern "C"
 
 #include "rt_ssim.hip"
+#include "rt_render_api.hip"

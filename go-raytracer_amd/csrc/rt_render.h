@@ -270,18 +270,9 @@ enum { PREF = 8 };  // u32 per prefix-count entry (RT_NUM_KINDS used, 16-B align
 // (node << 3) for an internal node, (first << 3) | count for a leaf of
 // `count` (1..4) consecutive bvh_geo records.
 enum { BN = 16, BVH_STACK = 64 };
-// 4-wide BVH (RT_BVH4, off): the binary tree collapsed one level (a node's
-// children are its binary children's children, or the binary child itself
-// when that is a leaf). Node: boxes as 6 x 4 floats (lo x y z, hi x y z;
-// SoA), child refs (int, -1 = empty slot, same encoding as above), the
-// smallest object index under each child; children sorted by that index.
-// Measured against the binary tree (same box, interleaved, parity green):
-// C4 4.20 vs 4.17 ms, C5 351 vs 317 ms serial (profiles/r04/bvh4/): half the
-// pops, but every visit tests four boxes and pushes up to four children.
-#ifndef RT_BVH4
-#define RT_BVH4 0
-#endif
-enum { BN4 = 32 };
+// (Measured and removed in round 5: a 4-wide BVH, C4 4.20 vs 4.17 ms, C5 351
+// vs 317 ms serial, profiles/r04/bvh4/; and a per-lane traversal fallback
+// after 256 wave node visits, C5 126.8 vs 113.2 ms, profiles/r04/bvhv/.)
 
 struct Ray {
   d3 o, d;
@@ -400,21 +391,6 @@ __device__ __forceinline__ LeafRec ld_leaf_p(PT p) {
 __device__ __forceinline__ LeafRec ld_leaf(const double* base, int j) {
   return ld_leaf_p((cdptr)base + (size_t)j * 16);  // wave-uniform j: scalar loads
 }
-// Per-lane BVH traversal (RT_BVH_LANE): the wave-coherent traversal visits the
-// union of its lanes' nodes, which for rays that thread the gaps of a dense
-// lattice (C5's horizon rows) grows to thousands of nodes per pass while each
-// ray alone visits a few hundred. After RT_BVH_LANE_AFTER wave node visits a
-// traversal hands its remaining stack entries to the lanes (each lane takes
-// the entries whose mask holds it, in stack order) and every lane finishes on
-// its own stack in private memory, with vector loads. The closest hit (ties on
-// the lowest index) and the lowest-index occluder do not depend on the visit
-// order, so results and counters are unchanged.
-#ifndef RT_BVH_LANE
-#define RT_BVH_LANE 0
-#endif
-#ifndef RT_BVH_LANE_AFTER
-#define RT_BVH_LANE_AFTER 256
-#endif
 // Index of the next record to prefetch, made to depend on the current record
 // (an empty asm that "reads" it): scalar loads return out of order, so the
 // only wait the compiler can emit is lgkmcnt(0); this places that wait before
@@ -1214,6 +1190,14 @@ __device__ __forceinline__ bool csg_hit_all_call(DP geo, IP kinds, IP code, int 
                                               double cut_lim, bool cut_strict) {
   return csg_hit_all(geo, kinds, code, nobj, g, r, t, face, cut_m, cut_lim, cut_strict);
 }
+// Callers pass a WAVE-UNIFORM composite g (every lane searches the same
+// composite): its fields are read through readfirstlane below. That holds
+// because composites never become BVH leaves (the host keeps them in the
+// unbounded-objects list, P.planes) and every other object loop is
+// wave-uniform; a per-lane object loop must not call this.
+// LF packs the leaf number in 8 bits (and the host's leaf groups use 0xff as
+// the end marker), hence:
+static_assert(RT_CSG_MAX_LEAVES < 255, "csg_hit packs leaf numbers in 8 bits");
 template <typename DP, typename IP, typename GP>
 __device__ __forceinline__ bool csg_hit(DP geo, IP kinds, IP code, int nobj,
                                         GP g, const Ray& r, double& t, int& face, double cut_m = 1.0,
@@ -1947,9 +1931,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (lane == 0 && n) atomicAdd(&cnt[k * WAVES_PER_WG + wave], (unsigned long long)n);
   };
   WaveStack bst;
-#if RT_BVH_LANE
-  int lst[BVH ? BVH_STACK : 1];  // per-lane BVH stack (private memory; see RT_BVH_LANE)
-#endif
   bst.mask = reinterpret_cast<uint64_t*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
   bst.ref = reinterpret_cast<int*>(smem + P.bvh_stack_off + WAVES_PER_WG * BVH_STACK * 8) + (threadIdx.x >> 6) * BVH_STACK;
 #ifdef RT_PHASE_TIMING
@@ -2675,66 +2656,11 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           }
 #else
         bst.push(ssp, lane, 0, wave_ballot(btr));
-#if RT_BVH_LANE && !RT_BVH4
-        int nvis = 0;
-#endif
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
           const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
-#if RT_BVH_LANE && !RT_BVH4
-          if (++nvis > RT_BVH_LANE_AFTER) {  // per-lane from here (see RT_BVH_LANE)
-            int lsp = 0;
-            bool ovf = false;
-            auto lpush = [&](int x) {
-              if (lsp < BVH_STACK)
-                lst[lsp++] = x;
-              else
-                ovf = true;
-            };
-            for (int e = 0; e <= ssp; e++) {  // (entry ssp: the one just popped)
-              const int re = __builtin_amdgcn_readfirstlane(bst.ref[e]);
-              const uint64_t me = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[e] >> 32)) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[e]);
-              if (btr && ((me >> lane) & 1)) lpush(re);
-            }
-            ssp = 0;
-            for (;;) {
-              const bool live = lsp > 0;
-              if (!wave_any(live)) break;
-              if (live) {
-                const int rl = lst[--lsp];
-                if (rl & 7) {
-                  const int first = rl >> 3, count = rl & 7;
-                  for (int j = first; j < first + count; j++) {
-                    const LeafRec L = ld_leaf_p(P.bvh_geo + (size_t)j * 16);  // vector loads
-                    const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
-                    if (may_hit_s(true, bof, df, tmax, L.cx, L.cy, L.cz, L.cr, bslack)) trace_exact(L.i, L.k, L.R.m, true);
-                  }
-                } else {
-                  const float* nb = P.bvh_nodes + (size_t)(rl >> 3) * BN;
-                  const int* ni = reinterpret_cast<const int*>(nb + 12);
-                  const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
-                  float t0 = 0.0f, t1 = 0.0f;
-                  const bool a0 = may_hit_box_a(true, bof, idf, bslack, tmax, nb, t0);
-                  const bool a1 = may_hit_box_a(true, bof, idf, bslack, tmax, nb + 6, t1);
-                  if (a0 && a1) {  // nearer child on top
-                    const bool c1n = t1 < t0;
-                    lpush(c1n ? ni[0] : ni[1]);
-                    lpush(c1n ? ni[1] : ni[0]);
-                  } else if (a0) {
-                    lpush(ni[0]);
-                  } else if (a1) {
-                    lpush(ni[1]);
-                  }
-                }
-              }
-            }
-            if (wave_any(ovf) && lane == 0) atomicAdd(P.stats + ST_WATCHDOG, 1ull);
-            break;
-          }
-#endif
 #endif
           const bool act = btr && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
@@ -2777,39 +2703,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               trace_exact(L.i, L.k, L.R.m, test);
             }
           } else {
-#if RT_BVH4
-            const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN4;  // scalar loads
-            const ciptr ni = (ciptr)(nb + 24);
-            const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
-            const int fl = __builtin_ctzll(m);  // the node's first lane: its entry distances order the children
-            uint64_t cm[4];
-            uint32_t ck[4];
-            int cr[4];
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-              cr[c] = ni[c];
-              float tn = 0.0f;
-              const bool a = may_hit_box6_a(act, bof, idf, bslack, tmax, nb[c], nb[4 + c], nb[8 + c], nb[12 + c],
-                                            nb[16 + c], nb[20 + c], tn);
-              cm[c] = cr[c] >= 0 ? wave_ballot(a) : 0ull;
-              ck[c] = f_order_key(__builtin_amdgcn_readlane(__float_as_int(tn), fl));
-            }
-            // push far to near: the nearest child is popped next
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-              int far = -1;
-              uint32_t fk = 0;
-#pragma unroll
-              for (int c = 0; c < 4; c++)
-                if (cm[c] && (far < 0 || ck[c] >= fk)) {
-                  far = c;
-                  fk = ck[c];
-                }
-              if (far < 0) break;
-              bst.push(ssp, lane, cr[far], cm[far]);
-              cm[far] = 0ull;
-            }
-#else
             const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN;  // scalar loads
             const ciptr ni = (ciptr)(nb + 12);
             const float tmax = found ? (float)(best_t - bt0) * 1.0001f + 1e-4f : 3.0e38f;
@@ -2829,7 +2722,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               if (m1) bst.push(ssp, lane, ni[1], m1);
               if (m0) bst.push(ssp, lane, ni[0], m0);
             }
-#endif
 #endif
           }
         }
@@ -3462,65 +3354,11 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           }
 #else
         bst.push(ssp, lane, 0, wave_ballot(sact));
-#if RT_BVH_LANE && !RT_BVH4
-        int nvis = 0;
-#endif
         while (ssp > 0) {
           ssp--;
           const int r = __builtin_amdgcn_readfirstlane(bst.ref[ssp]);
           const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[ssp] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[ssp]);
-#if RT_BVH_LANE && !RT_BVH4
-          if (++nvis > RT_BVH_LANE_AFTER) {  // per-lane from here (see RT_BVH_LANE)
-            int lsp = 0;
-            bool ovf = false;
-            auto lpush = [&](int x) {
-              if (lsp < BVH_STACK)
-                lst[lsp++] = x;
-              else
-                ovf = true;
-            };
-            for (int e = 0; e <= ssp; e++) {
-              const int re = __builtin_amdgcn_readfirstlane(bst.ref[e]);
-              const uint64_t me = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bst.mask[e] >> 32)) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)bst.mask[e]);
-              if (sact && ((me >> lane) & 1)) lpush(re);
-            }
-            ssp = 0;
-            for (;;) {
-              const bool live = lsp > 0;
-              if (!wave_any(live)) break;
-              if (live) {
-                const int rl = lst[--lsp];
-                if (rl & 7) {
-                  const int first = rl >> 3, count = rl & 7;
-                  for (int j = first; j < first + count; j++) {
-                    const LeafRec L = ld_leaf_p(P.bvh_geo + (size_t)j * 16);  // vector loads
-                    if (may_hit_s(L.i != hit_i && L.i < occ, sbof, sdf, sbtmax, L.cx, L.cy, L.cz, L.cr, sbslack))
-                      shadow_exact(L.i, L.k, L.R.m, true);
-                  }
-                } else {
-                  const float* nb = P.bvh_nodes + (size_t)(rl >> 3) * BN;
-                  const int* ni = reinterpret_cast<const int*>(nb + 12);
-                  float t0 = 0.0f, t1 = 0.0f;
-                  const bool a0 = may_hit_box_a(ni[2] < occ, sbof, sidf, sbslack, sbtmax, nb, t0);
-                  const bool a1 = may_hit_box_a(ni[3] < occ, sbof, sidf, sbslack, sbtmax, nb + 6, t1);
-                  if (a0 && a1) {  // lower-index subtree on top
-                    const bool c1f = ni[3] < ni[2];
-                    lpush(c1f ? ni[0] : ni[1]);
-                    lpush(c1f ? ni[1] : ni[0]);
-                  } else if (a0) {
-                    lpush(ni[0]);
-                  } else if (a1) {
-                    lpush(ni[1]);
-                  }
-                }
-              }
-            }
-            if (wave_any(ovf) && lane == 0) atomicAdd(P.stats + ST_WATCHDOG, 1ull);
-            break;
-          }
-#endif
 #endif
           const bool act = sact && ((m >> lane) & 1);
 #ifdef RT_PHASE_TIMING
@@ -3557,23 +3395,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               shadow_exact(L.i, L.k, L.R.m, test);
             }
           } else {
-#if RT_BVH4
-            // children in ascending smallest object index (host order): the
-            // lowest-index subtree is popped first, so it can prune the others
-            const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN4;  // scalar loads
-            const ciptr ni = (ciptr)(nb + 24);
-            uint64_t cm[4];
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-              float tn = 0.0f;
-              const bool a = may_hit_box6_a(CULL_AND(act, ni[4 + c] < occ), sbof, sidf, sbslack, sbtmax, nb[c],
-                                            nb[4 + c], nb[8 + c], nb[12 + c], nb[16 + c], nb[20 + c], tn);
-              cm[c] = ni[c] >= 0 ? wave_ballot(a) : 0ull;
-            }
-#pragma unroll
-            for (int c = 3; c >= 0; c--)
-              if (cm[c]) bst.push(ssp, lane, ni[c], cm[c]);
-#else
             const cfptr nb = (cfptr)P.bvh_nodes + (size_t)(r >> 3) * BN;  // scalar loads
             const ciptr ni = (ciptr)(nb + 12);
             float t0 = 0.0f, t1 = 0.0f;
@@ -3600,7 +3421,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               if (m1) bst.push(ssp, lane, ni[1], m1);
               if (m0) bst.push(ssp, lane, ni[0], m0);
             }
-#endif
 #endif
           }
         }

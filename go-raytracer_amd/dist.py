@@ -82,15 +82,26 @@ def gather_frame(buf, height, mode="bands", group=None, collective=None, slot=No
 
 class PendingGather:
     """An in-flight gather of one rank buffer (async_op): wait() completes it
-    and returns the assembled frame on rank 0 (None elsewhere)."""
+    and returns the assembled frame on rank 0 (None elsewhere). With `timing`
+    (a list), wait() appends (issue, done) CUDA events: issue recorded on the
+    launch stream when the gather was enqueued (= this rank's render end),
+    done on the caller's stream once the collective has completed -- their
+    difference is the gather's cost to this rank, waiting for the slowest
+    rank included."""
 
-    def __init__(self, work, stacked, height, mode, shape):
+    def __init__(self, work, stacked, height, mode, shape, issue=None, timing=None):
         self.work, self.stacked, self.height, self.mode, self.shape = work, stacked, height, mode, shape
+        self.issue, self.timing = issue, timing
 
     def wait(self):
         if self.work is not None:
             self.work.wait()
             self.work = None
+            if self.issue is not None and self.timing is not None:
+                import torch
+                done = torch.cuda.Event(enable_timing=True)
+                done.record()
+                self.timing.append((self.issue, done))
         if self.stacked is None:
             return None
         if self.mode == "interleaved":
@@ -98,20 +109,42 @@ class PendingGather:
         return self.stacked.reshape(-1, *self.shape[1:])[:self.height].clone()
 
 
-def gather_frame_async(buf, height, mode, slot, group=None):
+def gather_frame_async(buf, height, mode, slot, group=None, timing=None):
     """gather_frame as an async collective into receive slot `slot` (one
-    receive tensor per slot on rank 0, so two frames can be in flight)."""
+    receive tensor per slot on rank 0, so two frames can be in flight).
+    `timing`: see PendingGather (CUDA tensors only)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    issue = None
+    if timing is not None and buf.is_cuda:
+        issue = torch.cuda.Event(enable_timing=True)
+        issue.record()
     if dist.get_rank(group) == 0:
         key = (tuple(buf.shape), buf.dtype, buf.device, world, "slot", slot)
         stacked = _recv.get(key)
         if stacked is None:
             stacked = _recv[key] = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
         work = dist.gather(buf, gather_list=list(stacked.unbind(0)), dst=0, group=group, async_op=True)
-        return PendingGather(work, stacked, height, mode, tuple(buf.shape))
-    return PendingGather(dist.gather(buf, dst=0, group=group, async_op=True), None, height, mode, tuple(buf.shape))
+        return PendingGather(work, stacked, height, mode, tuple(buf.shape), issue, timing)
+    return PendingGather(dist.gather(buf, dst=0, group=group, async_op=True), None, height, mode, tuple(buf.shape),
+                         issue, timing)
+
+
+def rank_table(values, device=None):
+    """Every rank's list of floats, on every rank: [[rank 0's], [rank 1's], ...]
+    (one all_reduce of a zero-padded [world, n] tensor; identity without an
+    initialised process group). The N>1 bench line's per-rank telemetry."""
+    import torch
+    import torch.distributed as dist
+    vals = [float(v) for v in values]
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [vals]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = torch.zeros((world, len(vals)), dtype=torch.float64, device=device)
+    t[rank] = torch.tensor(vals, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()
 
 
 def reduce_max_sum(values, device=None):
@@ -193,6 +226,8 @@ class DistributedRenderer:
         self.bufs = [self.buf] + [torch.zeros_like(self.buf) for _ in range(nbufs - 1)]
         self.pending = [None] * nbufs
         self.k = 0
+        # (issue, done) event pairs of completed pipelined gathers (telemetry)
+        self.gather_events = []
 
     def has_work(self):
         if self.mode in ("frame", "band"):
@@ -243,7 +278,7 @@ class DistributedRenderer:
             if gather:
                 if self.pipeline:
                     # issued on the launch stream: the collective waits for this render only
-                    self.pending[slot] = gather_frame_async(buf, self.H, self.mode, slot)
+                    self.pending[slot] = gather_frame_async(buf, self.H, self.mode, slot, timing=self.gather_events)
                     return None  # the frame comes from flush() / a later step
                 self.frame = gather_frame(buf, self.H, self.mode, collective=collective,
                                           slot=slot if self.inflight > 1 else None)
@@ -252,6 +287,15 @@ class DistributedRenderer:
             # caller's stream (which reads it) is ordered after it
             torch.cuda.current_stream().wait_stream(stream)
         return self.frame
+
+    def gather_ms(self):
+        """Mean per-frame cost of the completed pipelined gathers to this rank
+        (ms from its render end to the collective's completion; None if no
+        timed gather ran); resets the record. Call after flush() and a sync."""
+        ev, self.gather_events = self.gather_events, []
+        if not ev:
+            return None
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
 
     def flush(self):
         """Complete every in-flight gather (pipeline mode); returns the frame of

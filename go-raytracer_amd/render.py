@@ -81,6 +81,8 @@ def load_library(path=None):
     l.rt_tile_order_info.restype = i
     l.rt_render.argtypes = [vp, vp, vp]
     l.rt_render.restype = i
+    l.rt_render_last_timing.argtypes = [vp]
+    l.rt_render_last_timing.restype = i
     if l.rt_abi_version() != abi.RT_ABI_VERSION:
         raise RenderError("librtamd ABI version mismatch")
     _lib = l

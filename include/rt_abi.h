@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 #define RT_EXP_AMD64_FMA 0
 #define RT_EXP_AMD64 1
 #define RT_EXP_PORTABLE 2
@@ -436,14 +436,42 @@ int rt_ssim_rgba8(rt_context *ctx, const uint8_t *d_a, const uint8_t *d_b, int w
                   double *out_ssim, void *stream);
 
 /* Convenience, synchronous whole-frame Render() into host memory
- * (width*height*4 bytes, caller-owned): the replacement of
- * func Render(*Scene) image.Image (raytracer.go:589-682). Uses a cached
- * context and device frame buffer per device, with scene specialisation
- * (rt_set_specialize: the first call with a new scene shape pays the hipRTC
- * compile, later ones reuse it; RT_RENDER_SPECIALIZE=0 in the environment
- * keeps the generic kernel). stats may be NULL. Includes the scene upload and
- * the PCIe transfer of the image. */
+ * (width*height*4 bytes, caller-owned, e.g. Go's image.RGBA.Pix): the
+ * replacement of func Render(*Scene) image.Image (raytracer.go:589-682).
+ * Keeps, per device, two contexts with the last scene (an unchanged scene --
+ * byte-equal arrays -- is not converted or uploaded again), a device frame
+ * and a pinned bounce buffer; renders the frame as row bands alternating over
+ * the two contexts and copies each finished band to rgba_out while later
+ * bands render. Scene specialisation (rt_set_specialize) is on: the first
+ * call with a new scene shape pays the hipRTC compile, later ones reuse it;
+ * if the compile fails the generic kernel renders the same pixels (logged
+ * once to stderr); RT_RENDER_SPECIALIZE=0 in the environment keeps the
+ * generic kernel. stats may be NULL; stats->kernel_ms is the GPU span of the
+ * frame. Includes the scene upload and the PCIe transfer of the image. */
 int rt_render(const rt_scene *scene, uint8_t *rgba_out, rt_stats *stats);
+
+/* ABI 5: the parts of the calling thread's last rt_render call, on one host
+ * timeline (setup + render_wait + copy_tail = total):
+ *   setup_ms        scene compare (and, if it changed, conversion, upload,
+ *                   specialisation, tile-cost estimate) and the launches
+ *   render_wait_ms  until the frame's last band has rendered (the earlier
+ *                   bands' host copies run inside it)
+ *   copy_tail_ms    the last band's DMA and host copy, and the counters
+ *   gpu_ms          GPU span of the frame (first band's start to last end)
+ * bands: row bands the frame was rendered in; scene_reused: the scene was
+ * unchanged; specialized: the specialised kernel rendered it. */
+typedef struct rt_render_timing {
+    double total_ms;
+    double setup_ms;
+    double render_wait_ms;
+    double copy_tail_ms;
+    double gpu_ms;
+    int32_t bands;
+    int32_t scene_reused;
+    int32_t specialized;
+    int32_t reserved;
+} rt_render_timing;
+int rt_render_last_timing(rt_render_timing *out);
 
 #ifdef __cplusplus
 }

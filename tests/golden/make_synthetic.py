@@ -42,6 +42,12 @@ FULL = {
     # whose shadow and reflection rays take the BVH culls' far-origin shift
     # (rt_render.h far_shift)
     "c5_7680x4320_rows2156-2164": ("c5", 7680, 4320, (2156, 2164)),
+    # the top of the frame (sky above the sphere field), the lower middle
+    # (ground reflections of the sphere field at depth 8, raytracer.go:512-528)
+    # and the bottom rows (the nearest ground, the steepest reflections)
+    "c5_7680x4320_rows0-8": ("c5", 7680, 4320, (0, 8)),
+    "c5_7680x4320_rows3200-3208": ("c5", 7680, 4320, (3200, 3208)),
+    "c5_7680x4320_rows4312-4320": ("c5", 7680, 4320, (4312, 4320)),
 }
 
 

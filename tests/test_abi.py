@@ -29,15 +29,15 @@ def test_library_exports_every_declared_symbol():
     lib = rt.load_library()
     for n in declared_functions():
         assert hasattr(lib, n), n
-    assert lib.rt_abi_version() == rt.abi.RT_ABI_VERSION == 4
+    assert lib.rt_abi_version() == rt.abi.RT_ABI_VERSION == 5
 
 
 def test_struct_layout_matches_header(tmp_path):
     prog = tmp_path / "layout.c"
     prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s"\n' % HEADER + r'''
 int main(void) {
-  printf("%zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_point_light), sizeof(rt_object),
-         sizeof(rt_scene), sizeof(rt_stats));
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_point_light), sizeof(rt_object),
+         sizeof(rt_scene), sizeof(rt_stats), sizeof(rt_render_timing));
   printf("%zu %zu %zu %zu\n", offsetof(rt_object, transform), offsetof(rt_object, plane_normal),
          offsetof(rt_scene, lights), offsetof(rt_scene, num_materials));
   return 0;
@@ -49,7 +49,7 @@ int main(void) {
     got = [int(v) for v in out]
     a = rt.abi
     want = [C.sizeof(a.rt_material), C.sizeof(a.rt_point_light), C.sizeof(a.rt_object), C.sizeof(a.rt_scene),
-            C.sizeof(a.rt_stats), a.rt_object.transform.offset, a.rt_object.plane_normal.offset,
+            C.sizeof(a.rt_stats), C.sizeof(a.rt_render_timing), a.rt_object.transform.offset, a.rt_object.plane_normal.offset,
             a.rt_scene.lights.offset, a.rt_scene.num_materials.offset]
     assert got == want
 

@@ -139,3 +139,36 @@ def test_reference_dice_program_renders_through_csg():
     packed = S.convert(args)
     img, st = oracle_bind.render_rows(packed)
     assert st.tests[rt.abi.RT_CSG] > 0 and (img[..., :3] > 0).any()
+
+
+def test_far_origin_hits_are_first_membership_changes():
+    """Rays starting 150-400 units out (the origins for which the device's
+    composite search shifts its culls, rt_render.h csg_hit RT_CSG_FAR) against
+    a composite of 20 leaves with a half-space and tied duplicate leaves: the
+    oracle's hit is still the first membership change along the ray."""
+    rng = random.Random(7)
+    body = S.Intersect(S.Cube(M).translate(-1.0, -1.0, -1.0).uscale(2.0), S.Plane(M).translate(0.0, 0.5, 0.0).rotatez(20.0))
+    sph = [S.Sphere(M).translate(-0.75 + 0.5 * i, -0.75 + 0.5 * j, -1.0).uscale(0.3) for i in range(4) for j in range(4)]
+    sph += [sph[3], sph[9]]
+    holes = sph[0]
+    for s in sph[1:]:
+        holes = S.union(holes, s)
+    solid = S.Difference(body, holes)
+    checked = 0
+    for _ in range(60):
+        r = rng.uniform(150.0, 400.0)
+        u = np.array([rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(-1, 1)])
+        o = r * u / np.linalg.norm(u)
+        target = np.array([rng.uniform(-0.9, 0.9), rng.uniform(-0.9, 0.9), rng.uniform(-1.0, 1.0)])
+        d = target - o
+        d /= np.linalg.norm(d)
+        ok, t, _ = _hit(solid, o, d)
+        tmin = r - 2.0  # the solid lies within |p| < 2
+        tmax = t if ok else r + 2.0
+        ts = np.linspace(tmin, tmax - 1e-6, 400)
+        states = {_inside(solid, o + s * d) for s in ts}
+        assert len(states) == 1, (o, d, t)
+        if ok:
+            assert _inside(solid, o + (t - 1e-7 * r) * d) != _inside(solid, o + (t + 1e-7 * r) * d)
+            checked += 1
+    assert checked > 20

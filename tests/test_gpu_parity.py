@@ -562,6 +562,54 @@ def test_specialised_full_4k_c3_equals_generic(ctx, spec_ctx):
     assert spec_ctx.specialized() == (True, 0.0)  # cached: no second compile
 
 
+def _csg_far_scene(width, height):
+    """A composite of 22 leaves -- cube, half-space plane leaf, 18 spheres of
+    which two are exact duplicates (tied intervals) and two sit behind --
+    raised above the horizon, with a low light behind the camera: the shadow
+    rays of ground points 100-300 units out cross the composite from
+    |origin| > 100, so the composite search's far-origin shift (rt_render.h
+    csg_hit, RT_CSG_FAR) and its spatial leaf groups (>= RT_CSG_GROUP_MIN
+    leaves; the plane in an unbounded group) both run. A mirror wall 300
+    units out closes the ground."""
+    glass = S.material((0.9, 1.0, 0.9), 0.2, 0.0, 0.8, 1.5, 0.5, 0.8, 60.0)
+    red = S.material((0.9, 0.3, 0.3), 0.2, 0.0, 0.0, 0.0, 0.9, 0.4, 10.0)
+    mirror = S.material((0.7, 0.7, 0.8), 0.8, 0.0, 0.0, 0.0, 0.3, 0.5, 20.0)
+    body = S.Intersect(S.Cube(red).translate(-1.0, 1.0, 5.0).uscale(2.0),
+                       S.Plane(red).translate(0.0, 2.5, 0.0).rotatez(20.0))
+    spheres = [S.Sphere(glass).translate(-0.75 + 0.5 * i, 1.25 + 0.5 * j, 5.0).uscale(0.3)
+               for i in range(4) for j in range(4)]
+    spheres += [spheres[5], spheres[10]]  # exact ties: identical leaves
+    spheres += [S.Sphere(glass).translate(0.2, 2.1, 7.0).uscale(0.45), S.Sphere(red).translate(-0.4, 1.7, 7.0).uscale(0.35)]
+    holes = spheres[0]
+    for sp in spheres[1:]:
+        holes = S.union(holes, sp)
+    comp = S.Difference(body, holes)
+    wall = S.Plane(mirror).translate(0.0, 0.0, 300.0).rotatex(-90.0)
+    ground = S.Plane(S.material((0.6, 0.6, 0.7), 0.3, 0.0, 0.0, 0.0, 1.0, 0.0, 1.0)).translate(0.0, -3.0, 0.0)
+    # the second light, low behind the camera: shadow rays from the ground
+    # 100-300 units out pass through the composite (raised above the horizon)
+    lights = [S.PointLight((4.0, 6.0, -2.0), (0.8, 0.8, 0.8)), S.PointLight((0.0, 4.0, -50.0), (0.5, 0.5, 0.6))]
+    return S.RenderArgs(ambient=(0.1, 0.1, 0.1), lights=lights, scene=S.union(S.union(comp, wall), ground),
+                        depth=5, fov=90.0, width=width, height=height)
+
+
+@pytest.mark.parametrize("kernel", ["generic", "specialised"])
+def test_csg_leaf_groups_and_far_origins_match_oracle(ctx, spec_ctx, kernel):
+    """the composite search's leaf groups (incl. a plane leaf and
+    tied leaves) and its far-origin shift against the oracle, bytes and
+    counters, in both kernels."""
+    packed = rt.scene.convert(_csg_far_scene(96, 64))
+    assert packed.scene.num_csg_leaves == 22
+    kinds = [packed.scene.csg_leaves[i].kind for i in range(22)]
+    assert rt.abi.RT_PLANE in kinds
+    c = ctx if kernel == "generic" else spec_ctx
+    img, st = render(c, packed)
+    ref, ost = oracle_bind.render_rows(packed)
+    assert_same(img, ref, "csg far/groups %s" % kernel)
+    assert st.as_dict() == ost.as_dict()
+    assert st.tests[rt.abi.RT_CSG] > 0
+
+
 def test_rt_render_repeated_calls_equal_oracle():
     """rt_render (the synchronous Render() seam, raytracer.go:589) called
     repeatedly from one process on alternating scenes: cached context and
