@@ -480,7 +480,7 @@ struct SpecKey {
   int pow_bits = 7;                      // unrolled specular powering steps
   int nocull = 0;                        // rt_set_accel without RT_ACCEL_CULL: -DRT_CULL=0
   int quads = 0;                         // pixel schedule: SCH_SERIAL / SCH_QUADS / SCH_PAIRS (pick_schedule)
-  int share = 0;                         // work sharing at the tail (rt_set_work_sharing): -DRT_SHARE=1
+  int share = 0;                         // work sharing at the tail (rt_set_work_sharing): -DRT_SHARE=<mode>
   int far = 1;                           // 0: -DRT_FAR_SHIFT=0 (BVH scenes below RT_FAR_MIN_OBJ objects)
   std::string str() const {
     return std::to_string(lds) + ":" + std::to_string(bvh) + ":" + std::to_string(csg) + ":" + std::to_string(nobj) + ":" + kinds + ":" +
@@ -529,7 +529,14 @@ struct rt_context {
   // tile is traced (estimate launch); launches then deal their tiles most
   // expensive first, so the end of a launch is made of cheap tiles.
   bool order_on = true;
-  bool share_on = false;  // rt_set_work_sharing (specialised kernels only)
+  int share_mode = 0;  // rt_set_work_sharing (specialised kernels only): RT_SHARE_GROUP / RT_SHARE_DEVICE
+  // device-wide sharing (RT_SHARE_DEVICE): slots per (wave slot, lane, level),
+  // the ring of posted slot ids and its head / tail tickets (rt_render.h gs_*)
+  uint64_t* gboard = nullptr;
+  uint64_t* gring = nullptr;
+  uint64_t* gctl = nullptr;
+  size_t gslots = 0;  // slots gboard holds (stack_waves * 64 * frames of its layout)
+  int gframes = 0;    // frames per lane of that layout
   unsigned int* est = nullptr;              // device: rays traced per frame tile
   size_t est_cap = 0;                       // tiles est can hold
   unsigned long long* est_stats = nullptr;  // the estimate launch's counters (discarded)
@@ -837,7 +844,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   if (sk.nlights > 0) defs.push_back("-DRT_SPEC_NLIGHTS=" + std::to_string(sk.nlights));
   defs.push_back("-DRT_SPEC_POWBITS=" + std::to_string(sk.pow_bits));
   if (sk.nocull) defs.push_back("-DRT_CULL=0");
-  if (sk.share) defs.push_back("-DRT_SHARE=1");
+  if (sk.share) defs.push_back("-DRT_SHARE=" + std::to_string(sk.share));
   if (sk.quads == SCH_PAIRS) defs.push_back("-DRT_PAIRS=1");
   if (!sk.far) defs.push_back("-DRT_FAR_SHIFT=0");
   std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
@@ -934,7 +941,7 @@ int spec_prepare(rt_context* c) {
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
   sk.quads = pick_schedule(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus, c->inflight, true);
-  sk.share = c->share_on ? 1 : 0;
+  sk.share = c->share_mode;
   if (sk.share && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the board assumes one owner lane per pixel
   c->spec_key = sk;
   for (auto& f : c->spec_alt_fn) f = nullptr;
@@ -1026,7 +1033,9 @@ int rt_scene_info(rt_context* c, int* flags) {
   const bool lds = scene_in_lds(s);
   *flags = (lds ? RT_INFO_LDS : 0) | (s.use_bvh ? RT_INFO_BVH : 0) | (s.has_csg ? RT_INFO_CSG : 0) |
            ((!lds && !s.use_bvh && !s.has_csg) ? RT_INFO_STREAM : 0) |
-           ((c->spec_fn && c->spec_key.share) ? RT_INFO_WAVEFRONT : 0) | (c->tile_cost.empty() ? 0 : RT_INFO_ORDERED);
+           ((c->spec_fn && c->spec_key.share) ? RT_INFO_WAVEFRONT : 0) |
+           ((c->spec_fn && c->spec_key.share == RT_SHARE_DEVICE) ? RT_INFO_SHARE_DEVICE : 0) |
+           (c->tile_cost.empty() ? 0 : RT_INFO_ORDERED);
   return RT_OK;
 }
 
@@ -1128,6 +1137,9 @@ void rt_destroy(rt_context* c) {
   clear_orders(c);
   (void)hipFree(c->est);
   (void)hipFree(c->est_stats);
+  (void)hipFree(c->gboard);
+  (void)hipFree(c->gring);
+  (void)hipFree(c->gctl);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -1796,7 +1808,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const bool quads = sch == SCH_QUADS || (sch == SCH_PAIRS && !spec);
   const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
   // the board is in LDS only for a kernel compiled with work sharing
-  const bool share = spec && c->spec_key.share;
+  const bool share = spec && c->spec_key.share == RT_SHARE_GROUP;  // (the device-wide board is in HBM)
   const int stream_off = board_off + (share ? BOARD_BYTES : 0);
   const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
@@ -1847,6 +1859,27 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   c->last_waves = grid * WAVES_PER_WG;
   c->launches++;
   if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
+  if (spec && c->spec_key.share == RT_SHARE_DEVICE) {
+    // device-wide board: zeroed (slots FREE, ring tickets 0) whenever its
+    // layout changes, so a stale ticket can only name a slot of this layout
+    const size_t need = (size_t)c->stack_waves * 64 * frames;
+    if (need != c->gslots || frames != c->gframes) {
+      (void)hipFree(c->gboard);
+      c->gboard = nullptr;
+      c->gslots = 0;
+      if (hipMalloc((void**)&c->gboard, need * GS_REC * sizeof(uint64_t)) != hipSuccess)
+        return fail(RT_E_NOMEM, "device-wide work-sharing slots");
+      if (!c->gring && hipMalloc((void**)&c->gring, (size_t)GS_RING * sizeof(uint64_t)) != hipSuccess)
+        return fail(RT_E_NOMEM, "device-wide work-sharing ring");
+      if (!c->gctl && hipMalloc((void**)&c->gctl, GS_CTL_U64 * sizeof(uint64_t)) != hipSuccess)
+        return fail(RT_E_NOMEM, "device-wide work-sharing control");
+      HIP_TRY(hipMemsetAsync(c->gboard, 0, need * GS_REC * sizeof(uint64_t), st));
+      HIP_TRY(hipMemsetAsync(c->gring, 0, (size_t)GS_RING * sizeof(uint64_t), st));
+      HIP_TRY(hipMemsetAsync(c->gctl, 0, GS_CTL_U64 * sizeof(uint64_t), st));
+      c->gslots = need;
+      c->gframes = frames;
+    }
+  }
   Params P;
   std::memset(&P, 0, sizeof P);
   P.lds_frames_off = frames_off;
@@ -1857,6 +1890,10 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.qmask_off = qmask_off;
   P.jump_off = jump_off;
   P.board_off = board_off;
+  P.gboard = c->gboard;
+  P.gring = c->gring;
+  P.gctl = c->gctl;
+  P.gslots = c->gslots;
   P.off_geo = s.off_geo;
   P.off_shade = s.off_shade;
   P.off_mats = s.off_mats;
@@ -2008,7 +2045,8 @@ static int estimate_costs(rt_context* c) {
 
 int rt_set_work_sharing(rt_context* c, int enable) {
   if (!c) return fail(RT_E_INVALID, "rt_set_work_sharing: NULL context");
-  c->share_on = enable != 0;
+  if (enable < 0 || enable > RT_SHARE_DEVICE) return fail(RT_E_INVALID, "rt_set_work_sharing: unknown mode");
+  c->share_mode = enable;
   return c->has_scene ? spec_prepare(c) : RT_OK;
 }
 
@@ -2062,6 +2100,7 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
     // reset would) so that later reads report later launches, then fail
     HIP_TRY(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st));
     HIP_TRY(hipMemsetAsync(c->stats_part, 0, part.size() * sizeof(unsigned long long), st));
+    c->gslots = 0;  // a stopped launch may leave device-wide board slots claimed: rebuilt at the next launch
     HIP_TRY(hipStreamSynchronize(st));
     c->primary_pending = 0;
     c->launches = 0;

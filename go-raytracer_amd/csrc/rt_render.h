@@ -246,7 +246,14 @@ struct Params {
   const double* arec;  // [nobj][AXIS_REC] compact records of axis-aligned spheres (runs with axis = 1)
   int cnt_off;    // LDS byte offset of the event counters (CNT_BYTES)
   int kind_mask;  // bit k: the scene has objects of kind k
-  int board_off;  // LDS byte offset of the work-sharing board (RT_SHARE)
+  int board_off;  // LDS byte offset of the work-sharing board (RT_SHARE == 1)
+  // device-wide work sharing (RT_SHARE == 2): slots [wave slot][lane][level]
+  // of GS_REC u64, the ring of posted slot ids (GS_RING), the ring's head and
+  // tail tickets (control block of GS_CTL_U64 u64)
+  uint64_t* gboard;
+  uint64_t* gring;
+  uint64_t* gctl;
+  unsigned long long gslots;  // slots gboard holds (a ticket naming another is ignored)
   // Tile order (host: scene-setup cost estimate, most expensive first): the
   // pool's virtual tile v renders tile order[v] of the launch; nullptr = in order
   const unsigned int* order;
@@ -1445,12 +1452,14 @@ __device__ __forceinline__ int core_gfield(int c) { return c < 3 ? c : (c == 3 ?
 
 // Frame flags (packed with the material index): packed = material << PK_MAT |
 // board slot << PK_SLOT | flags. FL_FORKED: the pending refraction child was
-// posted to the workgroup's board (slot PK_SLOT) for another lane to trace.
+// posted to the board (slot PK_SLOT: 24 bits, the device-wide board's slots
+// are per (wave slot, lane, level)) for another lane to trace.
 // FL_TASK: a sentinel below a claimed subtree -- its colour goes to slot
 // PK_SLOT (the subtree runs at its own absolute levels, so the depth limit
 // and the frame layout are those of the owner's tree).
 enum { FL_TMODE = 1, FL_HASR = 2, FL_HAST = 4, FL_STAGE = 8, FL_VMMAT = 16, FL_FORKED = 32, FL_TASK = 64 };
-enum { PK_SLOT = 8, PK_MAT = 16 };
+enum { PK_SLOT = 8, PK_MAT = 32 };
+#define PK_SLOT_OF(packed) ((int)(((packed) >> PK_SLOT) & 0xffffff))
 
 // ---------------------------------------------------------------------------
 // Work sharing at the tail of a launch (RT_SHARE). Once the queue is drained a
@@ -1558,6 +1567,67 @@ __device__ __forceinline__ uint64_t low_bits(uint64_t m, int n) {
     m ^= b;
   }
   return r;
+}
+
+// ---------------------------------------------------------------------------
+// Device-wide work sharing (RT_SHARE == 2). The workgroup board above lets an
+// idle lane take only its own group's work, and at the tail of a launch the
+// groups still running deep glass trees (raytracer.go:512-556: reflect +
+// refract at every level, up to 2^depth - 1 rays per sample) are few, while
+// every other group has left. Here any idle lane of any drained wave on the
+// device can take a posted refraction subtree:
+//   * slots in global memory, one per (wave slot, lane, level) -- a frame is
+//     posted at most once, so slot ids need no allocation; record = the
+//     pending refraction ray (o, d), the child's level, the state word;
+//   * a ring of posted slot ids with monotone 64-bit head / tail tickets (per
+//     context, never reset: a stale ticket names a slot whose state is no
+//     longer POSTED, and its claim just fails);
+//   * claim = CAS POSTED -> CLAIMED on the slot; the owner reclaims a slot
+//     nobody claimed with CAS POSTED -> FREE and traces it itself, or takes
+//     the delivered colour (DONE -> FREE), or waits (S_WAIT);
+//   * every access to the shared words is an agent-scope relaxed atomic (sc1:
+//     past the non-coherent L1 and the other XCDs' L2s, MI355X_MICROARCH.md
+//     "Valid forms": 8-B agent atomics both sides), and a writer drains its
+//     stores (s_waitcnt vmcnt(0)) before the state or ticket that publishes
+//     them.
+// Pixels and counters are those of the serial recursion: the owner combines
+// the child's colour at its own frame exactly as it would its own (the
+// reference's per-level clamp, raytracer.go:557-561).
+// ---------------------------------------------------------------------------
+enum { GS_FREE = 0, GS_POSTED = 1, GS_CLAIMED = 2, GS_DONE = 3, GS_REC = 8 /* u64 per slot */,
+       GS_RING = 1 << 20 /* ring entries (u64) */, GS_HEAD = 0, GS_TAIL = 16 /* u64 index in the control block */,
+       GS_CTL_U64 = 32, GS_NIDLE = 30, GS_ACTIVE = 31 /* u32 counters: QSTRIDE rows of the launch's queue set */ };
+#define RT_AG_SCOPE __HIP_MEMORY_SCOPE_AGENT
+__device__ __forceinline__ uint64_t gs_ld(uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, RT_AG_SCOPE); }
+__device__ __forceinline__ void gs_st(uint64_t* p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, RT_AG_SCOPE); }
+__device__ __forceinline__ unsigned int gs_ld32(unsigned int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, RT_AG_SCOPE);
+}
+// every store this lane issued has completed (before a publishing store)
+__device__ __forceinline__ void gs_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ bool gs_cas(uint64_t* p, uint64_t from, uint64_t to) {
+  return __hip_atomic_compare_exchange_strong(p, &from, to, __ATOMIC_RELAXED, __ATOMIC_RELAXED, RT_AG_SCOPE);
+}
+__device__ __forceinline__ uint64_t* gs_slot(uint64_t* board, int q) { return board + (size_t)q * GS_REC; }
+// owner: take back a slot nobody claimed
+__device__ __forceinline__ bool gs_reclaim(uint64_t* board, int q) { return gs_cas(gs_slot(board, q) + 7, GS_POSTED, GS_FREE); }
+__device__ __forceinline__ bool gs_done(uint64_t* board, int q) { return gs_ld(gs_slot(board, q) + 7) == GS_DONE; }
+// owner: the delivered colour (after gs_done); the slot is free again
+__device__ __forceinline__ d3 gs_take(uint64_t* board, int q) {
+  uint64_t* r = gs_slot(board, q);
+  const d3 c = mk(__longlong_as_double((long long)gs_ld(r)), __longlong_as_double((long long)gs_ld(r + 1)),
+                  __longlong_as_double((long long)gs_ld(r + 2)));
+  gs_st(r + 7, GS_FREE);
+  return c;
+}
+// helper: the subtree's colour into the slot, then DONE
+__device__ __forceinline__ void gs_deliver(uint64_t* board, int q, d3 c) {
+  uint64_t* r = gs_slot(board, q);
+  gs_st(r, (uint64_t)__double_as_longlong(c.x));
+  gs_st(r + 1, (uint64_t)__double_as_longlong(c.y));
+  gs_st(r + 2, (uint64_t)__double_as_longlong(c.z));
+  gs_drain();
+  gs_st(r + 7, GS_DONE);
 }
 
 
@@ -1729,7 +1799,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // per-wave unit counters: zeroed before the barrier (any wave's lane 0 adds)
   if (threadIdx.x < NUNIT * WAVES_PER_WG) reinterpret_cast<unsigned long long*>(smem + P.cnt_off)[threadIdx.x] = 0ull;
   Board* Bd = reinterpret_cast<Board*>(smem + P.board_off);
-  if constexpr (RT_SHARE) {
+  if constexpr (RT_SHARE == 1) {
     if (threadIdx.x == 0) {
       Bd->post = 0ull;
       Bd->done = 0ull;
@@ -1739,6 +1809,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (threadIdx.x < WAVES_PER_WG) Bd->wfree[threadIdx.x] = (1u << SLOTS_PER_WAVE) - 1u;
   }
   if (blockIdx.x == 0 && threadIdx.x < QHEADS) atomicExch(P.queue_next + threadIdx.x * QSTRIDE, 0u);
+  if constexpr (RT_SHARE == 2) {
+    static_assert(QHEADS <= GS_NIDLE, "device-wide sharing counters follow the queue heads");
+    // the next launch's idle-lane and active-wave counters start at zero;
+    // every wave of this launch counts itself active
+    if (blockIdx.x == 0 && threadIdx.x < 2) atomicExch(P.queue_next + (GS_NIDLE + threadIdx.x) * QSTRIDE, 0u);
+    if ((threadIdx.x & 63) == 0) atomicAdd(P.queue + GS_ACTIVE * QSTRIDE, 1u);
+  }
   if constexpr (LDS) {
     const int n16 = P.blob_bytes / 16;
     for (int i = threadIdx.x; i < n16; i += WG)
@@ -1966,8 +2043,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   // The board slot a waiting owner (S_WAIT) waits on: its posted sample
   // `sample` (at sp == 0), else the posted refraction child of frame sp - 1.
   auto wait_slot = [&]() -> int {
-    if (!QD && sp == 0) return lw_fork(Bd->lw[threadIdx.x], sample);
-    return (int)((__double_as_longlong(core_ld(sp - 1, 4)) >> PK_SLOT) & 63);
+    if (RT_SHARE == 1 && !QD && sp == 0) return lw_fork(Bd->lw[threadIdx.x], sample);
+    return PK_SLOT_OF(__double_as_longlong(core_ld(sp - 1, 4)));
   };
   // Serial samples: account sample `sample` onwards after the lane finished
   // the one before -- run it (own), take a helper's colour, reclaim a posted
@@ -2002,7 +2079,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         state = S_IDLE;
         return;
       }
-      if (!RT_SHARE || __builtin_expect(sample < lw_own_end(w), 1)) {
+      if (RT_SHARE != 1 || __builtin_expect(sample < lw_own_end(w), 1)) {
         need_gen = true;  // next sample ray, generated in one uniform block
         state = S_TRACE;
         return;
@@ -2059,7 +2136,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             packed = __double_as_longlong(core_ld(sp - 1, 4));
           int fl = (int)(packed & 0xff);
           if (RT_SHARE && __builtin_expect((fl & FL_TASK) != 0, 0)) {  // a claimed subtree is done: hand its colour to the owner
-            board_deliver(Bd, (int)((packed >> PK_SLOT) & 63), res);
+            if constexpr (RT_SHARE == 2)
+              gs_deliver(P.gboard, PK_SLOT_OF(packed), res);
+            else
+              board_deliver(Bd, PK_SLOT_OF(packed), res);
             sp = 0;
             state = S_IDLE;
             have_res = false;
@@ -2071,13 +2151,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             bool here = true;
             core_st(sp - 1, 4, __longlong_as_double(packed | FL_STAGE));
             if (RT_SHARE && __builtin_expect((fl & FL_FORKED) != 0, 0)) {
-              const int q = (int)((packed >> PK_SLOT) & 63);
-              if (board_reclaim(Bd, q)) {  // nobody took it: trace it here
+              const int q = PK_SLOT_OF(packed);
+              if (RT_SHARE == 2 ? gs_reclaim(P.gboard, q) : board_reclaim(Bd, q)) {  // nobody took it: trace it here
                 SHDIAG(SH_RECLAIM);
-                board_free(Bd, q);
-              } else if (board_done(Bd, q)) {
+                if (RT_SHARE == 1) board_free(Bd, q);
+              } else if (RT_SHARE == 2 ? gs_done(P.gboard, q) : board_done(Bd, q)) {
                 here = false;
-                res = board_take(Bd, q);  // the next round combines (FL_STAGE set)
+                res = RT_SHARE == 2 ? gs_take(P.gboard, q) : board_take(Bd, q);  // the next round combines (FL_STAGE set)
               } else {
                 SHDIAG(SH_WAIT);
                 here = false;
@@ -2152,8 +2232,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         // finish by taking helpers' colours, so any advancing holder flushes)
         if (RT_PIX_BATCH && wave_any(state == S_ADV && held_px != ~0u && (RT_SHARE || (!PR && sample == 4)))) flush_pixels();
         if (state == S_ADV) {
-          const uint32_t w = RT_SHARE ? Bd->lw[threadIdx.x] : 4u;
-          if (RT_SHARE && __builtin_expect(lw_task(w) >= 0, 0)) {
+          const uint32_t w = RT_SHARE == 1 ? Bd->lw[threadIdx.x] : 4u;
+          if (RT_SHARE == 1 && __builtin_expect(lw_task(w) >= 0, 0)) {
             board_deliver(Bd, lw_task(w), sum);
             Bd->lw[threadIdx.x] = 0u;
             state = S_IDLE;
@@ -2278,7 +2358,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           rng = pcg_jump(Pcg{0xDEADULL ^ (uint64_t)px, 0xBEEFULL ^ (uint64_t)(py - ry)}, jrows[ry * 4],
                          jrows[ry * 4 + 1], jrows[ry * 4 + 2], jrows[ry * 4 + 3]);
           sample = 0;
-          if (RT_SHARE) Bd->lw[threadIdx.x] = 1u;  // own_end = 1
+          if (RT_SHARE == 1) Bd->lw[threadIdx.x] = 1u;  // own_end = 1
           sum = mk(0, 0, 0);
           sp = 0;
           need_gen = true;
@@ -2317,19 +2397,182 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           rng = pcg_jump(s0, j[0], j[1], j[2], j[3]);
           sum = mk(0, 0, 0);
           sp = 0;
-          if (RT_SHARE) Bd->lw[threadIdx.x] = 4u;  // own_end = 4, nothing posted
+          if (RT_SHARE == 1) Bd->lw[threadIdx.x] = 4u;  // own_end = 4, nothing posted
           need_gen = true;
           state = S_TRACE;
         }
       }
       pool_next += take;
     }
-    if (RT_SHARE && !sh_live && !exhausted && (guard_iters & 3u) == 0u)
+    if (RT_SHARE == 1 && !sh_live && !exhausted && (guard_iters & 3u) == 0u)
       sh_live = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&Bd->nidle, __ATOMIC_RELAXED, RT_WG_SCOPE)) > 0;
+    if (RT_SHARE == 2 && !sh_live && !exhausted && (guard_iters & 7u) == 0u)
+      sh_live = __builtin_amdgcn_readfirstlane(lane == 0 ? (int)gs_ld32(P.queue + GS_NIDLE * QSTRIDE) : 0) > 0;
     if (RT_SHARE && !sh_live && exhausted) sh_live = true;
     if (RT_SHARE && !sh_live) {
       // steady state: the refill left no lane idle (else the queue is drained)
-    } else if constexpr (RT_SHARE) {
+    } else if constexpr (RT_SHARE == 2) {
+      // ---- device-wide work sharing (see gs_*) ----
+      unsigned int* g_nidle = P.queue + GS_NIDLE * QSTRIDE;
+      unsigned int* g_active = P.queue + GS_ACTIVE * QSTRIDE;
+      auto rfl64 = [](uint64_t v) {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+      };
+      // (a) waiting owners whose helper delivered resume (the TRACE pass
+      // takes the colour and combines it at the frame)
+      if (__builtin_expect(wave_any(state == S_WAIT), 0)) {
+        if (state == S_WAIT && gs_done(P.gboard, wait_slot())) state = S_RESUME;
+      }
+      // the launch's idle helper lanes and posted, unclaimed tickets
+      int nid = 0;
+      uint64_t gh = 0, gt = 0;
+      if (lane == 0) {
+        nid = (int)gs_ld32(g_nidle);
+        gh = gs_ld(P.gctl + GS_HEAD);
+        gt = gs_ld(P.gctl + GS_TAIL);
+      }
+      nid = __builtin_amdgcn_readfirstlane(nid);
+      gh = rfl64(gh);
+      gt = rfl64(gt);
+      const long long outstanding = (long long)(gt - gh);
+      // (b) owners post the pending refraction child of their shallowest
+      // binary frame (frames above a claimed subtree's sentinel only) while
+      // idle lanes anywhere on the device outnumber the posted tickets
+      const int want = nid - (int)min(outstanding, (long long)(1 << 30));
+      if (__builtin_expect(want > 0 && outstanding < GS_RING / 2, 0)) {
+        const bool busy_lane = state == S_TRACE || state == S_SHADE || state == S_WAIT;
+        int L = -1;
+        if (busy_lane)
+          for (int l = sp - 1; l >= 0; l--) {
+            const int f = (int)(__double_as_longlong(core_ld(l, 4)) & 0xff);
+            if (f & FL_TASK) break;
+            if ((f & (FL_HASR | FL_HAST | FL_STAGE | FL_FORKED)) == (FL_HASR | FL_HAST)) L = l;
+          }
+        const uint64_t cm = wave_ballot(L >= 0);
+        if (cm) {
+          const int npost = min((int)__popcll(cm), want);
+          const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned int)(cm >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned int)cm, 0u));
+          const bool post = L >= 0 && rk < npost;
+          int q = 0;
+          if (post) {
+            SHDIAG(SH_POST_T);
+            q = (wslot * 64 + lane) * P.frames + L;
+            uint64_t* r = gs_slot(P.gboard, q);
+            const double* e = ext(L);
+            const d3 o = ld3(e, 0), dd = ld3(e, 3);
+            gs_st(r + 0, (uint64_t)__double_as_longlong(o.x));
+            gs_st(r + 1, (uint64_t)__double_as_longlong(o.y));
+            gs_st(r + 2, (uint64_t)__double_as_longlong(o.z));
+            gs_st(r + 3, (uint64_t)__double_as_longlong(dd.x));
+            gs_st(r + 4, (uint64_t)__double_as_longlong(dd.y));
+            gs_st(r + 5, (uint64_t)__double_as_longlong(dd.z));
+            gs_st(r + 6, (uint64_t)(L + 1));
+            gs_drain();
+            gs_st(r + 7, GS_POSTED);
+            const long long pk = __double_as_longlong(core_ld(L, 4));
+            core_st(L, 4, __longlong_as_double(pk | FL_FORKED | ((long long)q << PK_SLOT)));
+          }
+          gs_drain();  // every posted slot's state has landed before its ticket
+          uint64_t t0 = 0;
+          if (lane == 0) t0 = __hip_atomic_fetch_add(P.gctl + GS_TAIL, (uint64_t)npost, __ATOMIC_RELAXED, RT_AG_SCOPE);
+          t0 = rfl64(t0);
+          if (post) {
+            const uint64_t t = t0 + (uint64_t)rk;
+            gs_st(P.gring + (t & (GS_RING - 1)), (t << 32) | (uint32_t)q);
+          }
+        }
+      }
+      // (c) idle lanes of a drained wave claim tickets
+      uint64_t il = exhausted ? wave_ballot(state == S_IDLE) : 0ull;
+      if (__builtin_expect(il != 0 && outstanding > 0 && !P.est_out, 0)) {
+        const int nil = (int)__popcll(il);
+        uint64_t h = 0;
+        int k = 0;
+        if (lane == 0) {
+          uint64_t hh = gh;
+          for (int tries = 0; tries < 4; tries++) {
+            const uint64_t tt = gs_ld(P.gctl + GS_TAIL);
+            const int kk = tt > hh ? (int)min((uint64_t)nil, tt - hh) : 0;
+            if (kk <= 0) break;
+            if (__hip_atomic_compare_exchange_strong(P.gctl + GS_HEAD, &hh, hh + (uint64_t)kk, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, RT_AG_SCOPE)) {
+              h = hh;
+              k = kk;
+              break;
+            }
+          }
+        }
+        h = rfl64(h);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k > 0) {
+          const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned int)(il >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned int)il, 0u));
+          if (state == S_IDLE && rk < k) {
+            const uint64_t t = h + (uint64_t)rk;
+            uint64_t e = 0;
+            // the poster writes the ticket's entry right after taking it
+            for (int w_ = 0; w_ < (1 << 14); w_++) {
+              e = gs_ld(P.gring + (t & (GS_RING - 1)));
+              if ((uint32_t)(e >> 32) == (uint32_t)t) break;
+              __builtin_amdgcn_s_sleep(1);
+            }
+            if ((uint32_t)(e >> 32) == (uint32_t)t && (uint32_t)e < P.gslots) {
+              const int q = (int)(uint32_t)e;
+              uint64_t* r = gs_slot(P.gboard, q);
+              if (gs_cas(r + 7, GS_POSTED, GS_CLAIMED)) {  // (else its owner took it back)
+                SHDIAG(SH_CLAIM);
+                ray.o = mk(__longlong_as_double((long long)gs_ld(r + 0)), __longlong_as_double((long long)gs_ld(r + 1)),
+                           __longlong_as_double((long long)gs_ld(r + 2)));
+                ray.d = mk(__longlong_as_double((long long)gs_ld(r + 3)), __longlong_as_double((long long)gs_ld(r + 4)),
+                           __longlong_as_double((long long)gs_ld(r + 5)));
+                const int m0 = (int)gs_ld(r + 6);
+                // a sentinel below the subtree (its colour goes to slot q); the
+                // subtree runs at its own absolute levels
+                core_st(m0 - 1, 4, __longlong_as_double((long long)FL_TASK | ((long long)q << PK_SLOT)));
+                sp = m0;
+                state = S_TRACE;
+              }
+            }
+          }
+          il = wave_ballot(state == S_IDLE);
+        }
+      }
+      // (d) bookkeeping: helpers available (idle lanes of drained waves),
+      // waves still busy
+      const int cur_idle = (exhausted && !P.est_out) ? (int)__popcll(il) : 0;
+      if (cur_idle != my_idle) {
+        if (lane == 0) atomicAdd(g_nidle, (unsigned int)(cur_idle - my_idle));
+        my_idle = cur_idle;
+      }
+      const bool busy = wave_any(state != S_IDLE);
+      if (busy != my_active) {
+        if (lane == 0) atomicAdd(g_active, busy ? 1u : 0xffffffffu);
+        my_active = busy;
+      }
+      if (__builtin_expect(!busy, 0)) {
+        // drained: stay while the launch may still post work; leave once no
+        // wave is busy -- a posted or claimed subtree's owner is busy until it
+        // has the colour, so then nothing is left to take (stale tickets of
+        // reclaimed slots may remain) -- or after RT_SHARE_SPINS idle rounds
+        const int na = __builtin_amdgcn_readfirstlane(lane == 0 ? (int)gs_ld32(g_active) : 0);
+        if (na == 0 || ++spins > RT_SHARE_SPINS) {
+#ifdef RT_PHASE_TIMING
+          if (lane == 0) atomicAdd(P.stats + ST_SHDIAG + SH_SPIN, (unsigned long long)spins);
+#endif
+          if (lane == 0 && my_idle) atomicAdd(g_nidle, (unsigned int)(-my_idle));
+          break;
+        }
+        __builtin_amdgcn_s_sleep(RT_SHARE_SLEEP);
+        continue;
+      }
+      spins = 0;
+      if (__builtin_expect(!wave_any(state == S_TRACE || state == S_SHADE || state == S_RESUME), 0)) {
+        __builtin_amdgcn_s_sleep(RT_SHARE_SLEEP / 4);  // only waiting (or quad-holding) lanes
+        continue;
+      }
+    } else if constexpr (RT_SHARE == 1) {
       // ---- work sharing within the workgroup (see Board) ----
       // (a) owners whose helper delivered take the colour; it is propagated
       // by the TRACE pass's unwind (a posted sample is added in sample order
@@ -2746,7 +2989,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         }
       }
       const bool resumed = RT_SHARE && state == S_RESUME;  // a waiting owner's helper delivered
-      if (__builtin_expect(resumed, 0)) res = board_take(Bd, wait_slot());  // (not tracing: pf is false)
+      if (__builtin_expect(resumed, 0))  // (not tracing: pf is false)
+        res = RT_SHARE == 2 ? gs_take(P.gboard, wait_slot()) : board_take(Bd, wait_slot());
       unwind((tr && !found) || resumed, res, pf, pf_packed, pf_lw, pf_kr);
       PH_MARK(3);
     }

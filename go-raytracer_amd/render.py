@@ -170,7 +170,9 @@ class RenderContext:
     def set_work_sharing(self, enable=True):
         """Work sharing at the tail of a launch (specialised kernel only;
         default off; identical pixels and counters). Applies at once."""
-        _check(self.lib.rt_set_work_sharing(self.handle, int(bool(enable))), "rt_set_work_sharing")
+        # True / 1: the workgroup board; 2 (abi.RT_SHARE_DEVICE): device-wide
+        mode = int(enable)
+        _check(self.lib.rt_set_work_sharing(self.handle, mode), "rt_set_work_sharing")
 
     def tile_order_info(self):
         """(active, estimate_ms): whether the current scene's launches use a

@@ -375,7 +375,7 @@ int rt_set_frames_in_flight(rt_context *ctx, int n);
  * reports whether an order is active and the estimate's wall time. */
 int rt_set_tile_order(rt_context *ctx, int enable);
 /* Work sharing at the tail of a launch (MI355X-specific; pixels and counters
- * are identical either way; default off). With enable != 0 the context's
+ * are identical either way; default off). With enable = RT_SHARE_GROUP the context's
  * specialised kernel (rt_set_specialize) is compiled with a per-workgroup
  * board in LDS: once the work queue is drained, a lane still tracing a pixel
  * posts the samples it has not started and the pending refraction children
@@ -384,6 +384,13 @@ int rt_set_tile_order(rt_context *ctx, int enable);
  * the reference's order. Off by default: its code costs every round of the
  * kernel more than the tail gains on the BASELINE configs.
  * Applies to the current scene at once. */
+#define RT_SHARE_OFF 0
+#define RT_SHARE_GROUP 1
+/* RT_SHARE_DEVICE (ABI 5): the board is device-wide, in HBM -- an idle lane
+ * of any drained wave on the device (any workgroup, any XCD) takes a posted
+ * refraction subtree; drained waves stay to help until no wave of the launch
+ * is busy. Subtrees only (no sample posting); pixel pairs run as quads. */
+#define RT_SHARE_DEVICE 2
 int rt_set_work_sharing(rt_context *ctx, int enable);
 /* Whether the current scene has a tile order, and the estimate's wall time
  * (ms) at scene setup. */
@@ -404,6 +411,7 @@ int rt_tile_order_info(rt_context *ctx, int *active, double *estimate_ms);
 #define RT_INFO_STREAM 8
 #define RT_INFO_WAVEFRONT 16
 #define RT_INFO_ORDERED 32
+#define RT_INFO_SHARE_DEVICE 64 /* the work-sharing board is device-wide (RT_SHARE_DEVICE) */
 int rt_scene_info(rt_context *ctx, int *flags);
 
 /* Whether the current scene runs a specialised kernel, and the compile time

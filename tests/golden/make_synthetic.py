@@ -46,6 +46,9 @@ FULL = {
     # (ground reflections of the sphere field at depth 8, raytracer.go:512-528)
     # and the bottom rows (the nearest ground, the steepest reflections)
     "c5_7680x4320_rows0-8": ("c5", 7680, 4320, (0, 8)),
+    # the upper sphere field (the nearest layer's top edge is near row 171,
+    # the farthest layer's near row 1508: rays from the sky through the field)
+    "c5_7680x4320_rows600-608": ("c5", 7680, 4320, (600, 608)),
     "c5_7680x4320_rows3200-3208": ("c5", 7680, 4320, (3200, 3208)),
     "c5_7680x4320_rows4312-4320": ("c5", 7680, 4320, (4312, 4320)),
 }

@@ -17,15 +17,18 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def ctxs():
     """generic kernel; specialised kernel; specialised kernel with work
-    sharing at the tail (rt_set_work_sharing)"""
+    sharing at the tail (rt_set_work_sharing), the workgroup board; the same
+    with the device-wide board (RT_SHARE_DEVICE)"""
     import torch
     assert torch.cuda.is_available()
     g = rt.RenderContext(0)
     s = rt.RenderContext(0, specialize=True)
     w = rt.RenderContext(0, specialize=True)
-    w.set_work_sharing(True)
-    yield g, s, w
-    for c in (g, s, w):
+    w.set_work_sharing(rt.abi.RT_SHARE_GROUP)
+    d = rt.RenderContext(0, specialize=True)
+    d.set_work_sharing(rt.abi.RT_SHARE_DEVICE)
+    yield g, s, w, d
+    for c in (g, s, w, d):
         c.close()
 
 
@@ -63,6 +66,9 @@ def test_tile_order_and_sharing_match_oracle(ctxs, case):
     ref, ost = oracle_bind.render_rows(packed)
     ctxs[2].set_scene(packed)
     assert ctxs[2].scene_info() & rt.abi.RT_INFO_WAVEFRONT
+    assert not ctxs[2].scene_info() & rt.abi.RT_INFO_SHARE_DEVICE
+    ctxs[3].set_scene(packed)
+    assert ctxs[3].scene_info() & rt.abi.RT_INFO_SHARE_DEVICE
     ctxs[1].set_scene(packed)
     assert not ctxs[1].scene_info() & rt.abi.RT_INFO_WAVEFRONT
     for c in ctxs:
@@ -100,13 +106,13 @@ def test_cost_estimate_leaves_counters_alone(ctxs):
     assert st.as_dict() == ost.as_dict()
 
 
-@pytest.mark.parametrize("which", ["share", "pairs"])
+@pytest.mark.parametrize("which", ["share", "device", "pairs"])
 def test_interleaved_shares_with_order_match_full_frame(ctxs, which):
     """Strong-scaling shares (tile rows r, r + N, ...) each get their own
     tile order; gathered, they are the oracle's frame (with work sharing, and
     in the pixel-pairs schedule)."""
     import torch
-    s = ctxs[2] if which == "share" else ctxs[1]
+    s = {"share": ctxs[2], "device": ctxs[3], "pairs": ctxs[1]}[which]
     s.set_schedule(rt.abi.RT_SCHED_PAIRS if which == "pairs" else rt.abi.RT_SCHED_AUTO)
     args = rt.configs.c4(width=160, height=96)
     packed = rt.scene.convert(args)
@@ -195,6 +201,44 @@ def test_frames_in_flight_shares_keep_bytes_and_counters(cfg, world):
             outs.append((buf.cpu().numpy(), c.read_stats(reset=True).as_dict()))
         assert_same(outs[1][0], outs[0][0], "%s rank 0 of %d: pairs vs quads" % (cfg, world))
         assert outs[1][1] == outs[0][1]
+    finally:
+        a.close()
+        b.close()
+
+
+def test_device_sharing_full_c4csg_frame_and_shares():
+    """Config 4 as stated (c4csg: cube minus 64 spheres, 4K, depth 8) with the
+    device-wide board: the whole frame and each of the 8 interleaved
+    strong-scaling shares (where most lanes are idle early and nearly every
+    pending refraction subtree is posted) equal the unshared specialised
+    kernel's -- byte for byte, counter for counter; that kernel's full frame
+    is pinned against the oracle in test_gpu_parity.py."""
+    import torch
+    packed = rt.scene.convert(rt.configs.c4csg())
+    a = rt.RenderContext(0, specialize=True)
+    b = rt.RenderContext(0, specialize=True)
+    try:
+        b.set_work_sharing(rt.abi.RT_SHARE_DEVICE)
+        for c in (a, b):
+            c.set_scene(packed)
+        assert b.scene_info() & rt.abi.RT_INFO_SHARE_DEVICE
+        ref, st_ref = render(a, packed)
+        img, st = render(b, packed)
+        assert_same(img, ref, "c4csg device sharing, whole frame")
+        assert st.as_dict() == st_ref.as_dict()
+        world = 8
+        nt, K = rt.dist.tile_rows(packed.height, world)
+        for r in range(world):
+            n = max(0, min(K, (nt - r + world - 1) // world))
+            outs = []
+            for c in (a, b):
+                c.read_stats(reset=True)
+                buf = torch.zeros((n * 8, packed.width, 4), dtype=torch.uint8, device="cuda:0")
+                c.render_tile_rows_async(r, world, n, buf)
+                torch.cuda.synchronize()
+                outs.append((buf.cpu().numpy(), c.read_stats(reset=True).as_dict()))
+            assert_same(outs[1][0], outs[0][0], "c4csg share %d of %d, device sharing" % (r, world))
+            assert outs[1][1] == outs[0][1]
     finally:
         a.close()
         b.close()
