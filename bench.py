@@ -74,9 +74,11 @@ def parse():
                    help="rt_set_schedule: how pixels are dealt to lanes (identical pixels and counters); "
                         "auto picks from depth, pixels per lane and frames in flight. The PMC passes run "
                         "--inflight 1 with the schedule the in-flight bench picks")
-    p.add_argument("--work-sharing", choices=["on", "group", "device", "off"], default="off",
+    p.add_argument("--work-sharing", choices=["auto", "on", "group", "device", "off"], default="auto",
                    help="rt_set_work_sharing: tail work sharing compiled into the specialised kernel "
-                        "(on = group: a per-workgroup LDS board; device: a device-wide board in HBM)")
+                        "(on = group: a per-workgroup LDS board; device: a device-wide board in HBM; "
+                        "auto, the library default: device for CSG scenes at depth >= 7 on strong-scaling "
+                        "shares or without frames in flight)")
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
@@ -246,11 +248,11 @@ def gpu_span_ms(evs):
     return span / len(evs)
 
 
-def make_contexts(pkg, dev, packed, n, specialize, accel=None, schedule="auto", sharing=0):
+def make_contexts(pkg, dev, packed, n, specialize, accel=None, schedule="auto", sharing=None):
     ctxs = []
     for _ in range(n):
         c = pkg.RenderContext(dev.index, specialize=specialize)
-        if sharing:
+        if sharing is not None:  # (None: the library's default, RT_SHARE_AUTO)
             c.set_work_sharing(int(sharing))
         if accel is not None:
             c.set_accel(accel)
@@ -382,7 +384,7 @@ def main():
         raise SystemExit("--inflight must be >= 1")
     ctxs = make_contexts(pkg, dev, packed, args.inflight, args.specialize == "on",
                          accel=0 if args.accel == "none" else None, schedule=args.schedule,
-                         sharing={"off": 0, "on": 1, "group": 1, "device": 2}[args.work_sharing])
+                         sharing={"auto": None, "off": 0, "on": 1, "group": 1, "device": 2}[args.work_sharing])
     ctx = ctxs[0]
     spec_active, spec_ms = ctx.specialized()
     order_active, order_ms = ctx.tile_order_info()

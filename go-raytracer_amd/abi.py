@@ -25,7 +25,7 @@ RT_ACCEL_BVH, RT_ACCEL_CULL = 1, 2  # rt_set_accel flags
 RT_SCHED_AUTO, RT_SCHED_PIXEL, RT_SCHED_QUADS, RT_SCHED_PAIRS = 0, 1, 2, 3  # rt_set_schedule modes
 RT_INFO_LDS, RT_INFO_BVH, RT_INFO_CSG, RT_INFO_STREAM, RT_INFO_WAVEFRONT, RT_INFO_ORDERED = 1, 2, 4, 8, 16, 32  # rt_scene_info
 RT_INFO_SHARE_DEVICE = 64
-RT_SHARE_OFF, RT_SHARE_GROUP, RT_SHARE_DEVICE = 0, 1, 2  # rt_set_work_sharing
+RT_SHARE_OFF, RT_SHARE_GROUP, RT_SHARE_DEVICE, RT_SHARE_AUTO = 0, 1, 2, 3  # rt_set_work_sharing
 
 
 def RT_SPEC_LIGHTS(n):

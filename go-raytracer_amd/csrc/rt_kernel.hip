@@ -529,7 +529,7 @@ struct rt_context {
   // tile is traced (estimate launch); launches then deal their tiles most
   // expensive first, so the end of a launch is made of cheap tiles.
   bool order_on = true;
-  int share_mode = 0;  // rt_set_work_sharing (specialised kernels only): RT_SHARE_GROUP / RT_SHARE_DEVICE
+  int share_mode = RT_SHARE_AUTO;  // rt_set_work_sharing (specialised kernels only)
   // device-wide sharing (RT_SHARE_DEVICE): slots per (wave slot, lane, level),
   // the ring of posted slot ids and its head / tail tickets (rt_render.h gs_*)
   uint64_t* gboard = nullptr;
@@ -547,7 +547,7 @@ struct rt_context {
   bool specialize = false;
   int accel = RT_ACCEL_BVH | RT_ACCEL_CULL;  // rt_set_accel
   hipFunction_t spec_fn = nullptr;  // specialised kernel of the current scene, if any
-  hipFunction_t spec_alt_fn[3] = {nullptr, nullptr, nullptr};  // ... for the other pixel schedules (spec_for)
+  std::map<int, hipFunction_t> spec_alt;  // ... for other (schedule, work sharing) pairs (spec_for)
   SpecKey spec_key;                     // what spec_fn was compiled for
   double spec_ms = 0;               // hipRTC compile time of spec_fn (0 = cache hit)
 };
@@ -787,6 +787,21 @@ bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus, int infli
 // frame 4.15 vs 4.25 serial, over 2 ranks 2.08 vs 2.46 quads; over 4,
 // 10 px/lane, quads 1.16 vs 1.39).
 enum { SCH_SERIAL = 0, SCH_QUADS = 1, SCH_PAIRS = 2 };
+// Work sharing of a launch (SpecKey.share; specialised kernels only).
+// RT_SHARE_AUTO (the default) takes the device-wide board (rt_render.h gs_*)
+// for CSG scenes of depth >= 7 on launches that leave deep glass trees alone
+// at the end: strong-scaling shares (< 16 pixels per lane) and launches
+// without frames in flight. c4csg (cube - 64 spheres, 4K, depth 8; ms,
+// profiles/r05/gshare/): 8-rank share (two in flight) 4.52 -> 2.24, whole
+// frame serially 14.07 -> 11.5, but two whole frames in flight 10.63 ->
+// 11.00 (the board's polling and posting cost more than the overlapped tail
+// gains), so those keep it off.
+int pick_share(int mode, const DevScene& s, uint64_t pixels, int cus, int inflight) {
+  if (mode != RT_SHARE_AUTO) return mode;
+  const double ppl = (double)pixels / ((double)std::max(1, cus) * 4 * 3 * 64);  // pixels per lane
+  return (s.has_csg && s.depth >= 7 && (inflight <= 1 || ppl < 16.0)) ? RT_SHARE_DEVICE : RT_SHARE_OFF;
+}
+
 int pick_schedule(int sched, const DevScene& s, uint64_t pixels, int cus, int inflight, bool spec) {
   static const int env = getenv("RT_PIXEL_PAIRS") ? atoi(getenv("RT_PIXEL_PAIRS")) : -1;
   if (env > 0 || sched == RT_SCHED_PAIRS) return SCH_PAIRS;
@@ -941,31 +956,37 @@ int spec_prepare(rt_context* c) {
   if (!spec_key(c->sc, &sk)) return RT_OK;
   sk.nocull = (c->accel & RT_ACCEL_CULL) ? 0 : 1;
   sk.quads = pick_schedule(c->sched, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus, c->inflight, true);
-  sk.share = c->share_mode;
-  if (sk.share && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the board assumes one owner lane per pixel
+  sk.share = pick_share(c->share_mode, c->sc, (uint64_t)c->sc.width * c->sc.height, c->cus, c->inflight);
+  if (sk.share == RT_SHARE_GROUP && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the LDS board assumes one owner lane per pixel
   c->spec_key = sk;
-  for (auto& f : c->spec_alt_fn) f = nullptr;
+  c->spec_alt.clear();
   std::lock_guard<std::mutex> lock(g_spec_mu);
   return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
 }
 
-// The specialised kernel for `quads` (the scene's other schedule is compiled
-// on first use: a launch covering a small share of the frame).
-int spec_for(rt_context* c, int sch, hipFunction_t* fn) {
-  if (c->spec_fn && c->spec_key.share && sch == SCH_PAIRS) sch = SCH_QUADS;
-  if (!c->spec_fn || c->spec_key.quads == sch) {
+// The specialised kernel for schedule `sch` and work-sharing mode `share`
+// (another pair than the scene's is compiled on first use: a launch covering
+// a small share of the frame).
+int spec_for(rt_context* c, int sch, int share, hipFunction_t* fn) {
+  if (share == RT_SHARE_GROUP && sch == SCH_PAIRS) sch = SCH_QUADS;
+  if (!c->spec_fn || (c->spec_key.quads == sch && c->spec_key.share == share)) {
     *fn = c->spec_fn;
     return RT_OK;
   }
-  if (!c->spec_alt_fn[sch]) {
+  const int k = sch * 4 + share;
+  auto it = c->spec_alt.find(k);
+  if (it == c->spec_alt.end()) {
     SpecKey sk = c->spec_key;
     sk.quads = sch;
+    sk.share = share;
     double ms = 0;
+    hipFunction_t f = nullptr;
     std::lock_guard<std::mutex> lock(g_spec_mu);
-    int rc = spec_build(c->device, sk, &c->spec_alt_fn[sch], &ms);
+    int rc = spec_build(c->device, sk, &f, &ms);
     if (rc != RT_OK) return rc;
+    it = c->spec_alt.emplace(k, f).first;
   }
-  *fn = c->spec_alt_fn[sch];
+  *fn = it->second;
   return RT_OK;
 }
 
@@ -1799,16 +1820,18 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
   const int sch =
       est ? (int)SCH_SERIAL : pick_schedule(c->sched, s, launch_pixels, c->cus, c->inflight, c->spec_fn != nullptr);
-  hipFunction_t spec = nullptr;  // built for this scene's flavour (spec_key), this schedule
+  // (the estimate launch runs the scene's own sharing mode: no extra compile)
+  const int share_m = c->spec_fn ? (est ? c->spec_key.share : pick_share(c->share_mode, s, launch_pixels, c->cus, c->inflight)) : 0;
+  hipFunction_t spec = nullptr;  // built for this scene's flavour (spec_key), this schedule and sharing
   {
-    int rc = spec_for(c, sch, &spec);
+    int rc = spec_for(c, sch, share_m, &spec);
     if (rc != RT_OK) return rc;
   }
   // the generic kernels have no pairs flavour: quads instead (same pixels)
   const bool quads = sch == SCH_QUADS || (sch == SCH_PAIRS && !spec);
   const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
   // the board is in LDS only for a kernel compiled with work sharing
-  const bool share = spec && c->spec_key.share == RT_SHARE_GROUP;  // (the device-wide board is in HBM)
+  const bool share = spec && share_m == RT_SHARE_GROUP;  // (the device-wide board is in HBM)
   const int stream_off = board_off + (share ? BOARD_BYTES : 0);
   const int frames_off = stream_off + (use_stream ? WAVES_PER_WG * SCH * (GEO * (int)sizeof(double) + (int)sizeof(int)) : 0);
   int shmem = frames_off;
@@ -1859,7 +1882,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   c->last_waves = grid * WAVES_PER_WG;
   c->launches++;
   if (grid * WAVES_PER_WG > c->stack_waves) return fail(RT_E_INVALID, "frame stack smaller than the grid");
-  if (spec && c->spec_key.share == RT_SHARE_DEVICE) {
+  if (spec && share_m == RT_SHARE_DEVICE) {
     // device-wide board: zeroed (slots FREE, ring tickets 0) whenever its
     // layout changes, so a stale ticket can only name a slot of this layout
     const size_t need = (size_t)c->stack_waves * 64 * frames;
@@ -1867,11 +1890,15 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
       (void)hipFree(c->gboard);
       c->gboard = nullptr;
       c->gslots = 0;
-      if (hipMalloc((void**)&c->gboard, need * GS_REC * sizeof(uint64_t)) != hipSuccess)
+      // uncached (no XCD's L2 may hold a stale copy: rt_render.h gs_*)
+      if (hipExtMallocWithFlags((void**)&c->gboard, need * GS_REC * sizeof(uint64_t), hipDeviceMallocUncached) !=
+          hipSuccess)
         return fail(RT_E_NOMEM, "device-wide work-sharing slots");
-      if (!c->gring && hipMalloc((void**)&c->gring, (size_t)GS_RING * sizeof(uint64_t)) != hipSuccess)
+      if (!c->gring && hipExtMallocWithFlags((void**)&c->gring, (size_t)GS_RING * sizeof(uint64_t),
+                                             hipDeviceMallocUncached) != hipSuccess)
         return fail(RT_E_NOMEM, "device-wide work-sharing ring");
-      if (!c->gctl && hipMalloc((void**)&c->gctl, GS_CTL_U64 * sizeof(uint64_t)) != hipSuccess)
+      if (!c->gctl && hipExtMallocWithFlags((void**)&c->gctl, GS_CTL_U64 * sizeof(uint64_t), hipDeviceMallocUncached) !=
+                          hipSuccess)
         return fail(RT_E_NOMEM, "device-wide work-sharing control");
       HIP_TRY(hipMemsetAsync(c->gboard, 0, need * GS_REC * sizeof(uint64_t), st));
       HIP_TRY(hipMemsetAsync(c->gring, 0, (size_t)GS_RING * sizeof(uint64_t), st));
@@ -1894,6 +1921,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.gring = c->gring;
   P.gctl = c->gctl;
   P.gslots = c->gslots;
+  P.gset = c->qset;  // (alternates with the queue sets)
   P.off_geo = s.off_geo;
   P.off_shade = s.off_shade;
   P.off_mats = s.off_mats;
@@ -2045,7 +2073,7 @@ static int estimate_costs(rt_context* c) {
 
 int rt_set_work_sharing(rt_context* c, int enable) {
   if (!c) return fail(RT_E_INVALID, "rt_set_work_sharing: NULL context");
-  if (enable < 0 || enable > RT_SHARE_DEVICE) return fail(RT_E_INVALID, "rt_set_work_sharing: unknown mode");
+  if (enable < 0 || enable > RT_SHARE_AUTO) return fail(RT_E_INVALID, "rt_set_work_sharing: unknown mode");
   c->share_mode = enable;
   return c->has_scene ? spec_prepare(c) : RT_OK;
 }

@@ -253,6 +253,7 @@ struct Params {
   uint64_t* gboard;
   uint64_t* gring;
   uint64_t* gctl;
+  int gset;  // this launch's counter set (0 / 1); it zeroes the other
   unsigned long long gslots;  // slots gboard holds (a ticket naming another is ignored)
   // Tile order (host: scene-setup cost estimate, most expensive first): the
   // pool's virtual tile v renders tile order[v] of the launch; nullptr = in order
@@ -1585,18 +1586,34 @@ __device__ __forceinline__ uint64_t low_bits(uint64_t m, int n) {
 //   * claim = CAS POSTED -> CLAIMED on the slot; the owner reclaims a slot
 //     nobody claimed with CAS POSTED -> FREE and traces it itself, or takes
 //     the delivered colour (DONE -> FREE), or waits (S_WAIT);
-//   * every access to the shared words is an agent-scope relaxed atomic (sc1:
-//     past the non-coherent L1 and the other XCDs' L2s, MI355X_MICROARCH.md
-//     "Valid forms": 8-B agent atomics both sides), and a writer drains its
-//     stores (s_waitcnt vmcnt(0)) before the state or ticket that publishes
-//     them.
+//   * the board lives in UNCACHED device memory (hipDeviceMallocUncached:
+//     no XCD's L2 keeps a copy -- with ordinary memory the zeroing memset
+//     left clean lines in some L2s, and sc1 polls served from them never saw
+//     another XCD's update: idle waves spun to their limit, 8-rank c4csg
+//     shares took 140 ms instead of 5); every access to the shared words is
+//     an agent-scope relaxed atomic (sc1, past the CU's L1), and a writer
+//     drains its stores (s_waitcnt vmcnt(0)) before the state or ticket that
+//     publishes them. The launch's idle-lane and active-wave counters are in
+//     the same block (two sets, launches alternate, each zeroing the next).
 // Pixels and counters are those of the serial recursion: the owner combines
 // the child's colour at its own frame exactly as it would its own (the
 // reference's per-level clamp, raytracer.go:557-561).
 // ---------------------------------------------------------------------------
+#ifndef RT_GS_MIN_LEVELS
+#define RT_GS_MIN_LEVELS 3  // post only refraction children with >= this many levels below them
+#endif
 enum { GS_FREE = 0, GS_POSTED = 1, GS_CLAIMED = 2, GS_DONE = 3, GS_REC = 8 /* u64 per slot */,
-       GS_RING = 1 << 20 /* ring entries (u64) */, GS_HEAD = 0, GS_TAIL = 16 /* u64 index in the control block */,
-       GS_CTL_U64 = 32, GS_NIDLE = 30, GS_ACTIVE = 31 /* u32 counters: QSTRIDE rows of the launch's queue set */ };
+       GS_RING = 1 << 20 /* ring entries (u64) */,
+       // control block (u64 indices; the words 4 KB apart, so no two share a
+       // memory channel): ring head / tail, then two counter sets
+       GS_HEAD = 0, GS_TAIL = 512, GS_SET = 1024 /* set s at GS_SET + GS_SETSZ * s */, GS_SETSZ = 1536,
+       GS_NIDLE = 0, GS_ACTIVE = 512, GS_HELPERS = 1024 /* u64 in a set */, GS_CTL_U64 = GS_SET + 2 * GS_SETSZ };
+#ifndef RT_GS_POLL
+#define RT_GS_POLL 15  // a busy wave reads the board's words every (RT_GS_POLL + 1)-th round
+#endif
+#ifndef RT_GS_HELPERS
+#define RT_GS_HELPERS 16  // drained waves that stay to help (device-wide); the others leave at once
+#endif
 #define RT_AG_SCOPE __HIP_MEMORY_SCOPE_AGENT
 __device__ __forceinline__ uint64_t gs_ld(uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, RT_AG_SCOPE); }
 __device__ __forceinline__ void gs_st(uint64_t* p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, RT_AG_SCOPE); }
@@ -1779,7 +1796,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   constexpr bool PR = false;
 #else
   constexpr bool QD = QUADS;
-  constexpr bool PR = !QUADS && RT_PAIRS && !RT_SHARE;  // pixel pairs (the board assumes one owner lane)
+  constexpr bool PR = !QUADS && RT_PAIRS && RT_SHARE != 1;  // pixel pairs (the workgroup board assumes one owner lane)
 #endif
   // pixels per dequeue: 16 quads, 32 pairs (an 8x4 half tile) or 64 pixels
   constexpr unsigned int QCHUNK = QD ? 16u : PR ? 32u : (unsigned int)RT_QCHUNK_PIXEL;
@@ -1809,13 +1826,23 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (threadIdx.x < WAVES_PER_WG) Bd->wfree[threadIdx.x] = (1u << SLOTS_PER_WAVE) - 1u;
   }
   if (blockIdx.x == 0 && threadIdx.x < QHEADS) atomicExch(P.queue_next + threadIdx.x * QSTRIDE, 0u);
+  // device-wide sharing: this launch's idle-lane / active-wave counters
+  unsigned int* g_nidle = reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * P.gset + GS_NIDLE);
+  unsigned int* g_active = reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * P.gset + GS_ACTIVE);
+  unsigned int* g_helpers = reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * P.gset + GS_HELPERS);
   if constexpr (RT_SHARE == 2) {
-    static_assert(QHEADS <= GS_NIDLE, "device-wide sharing counters follow the queue heads");
-    // the next launch's idle-lane and active-wave counters start at zero;
-    // every wave of this launch counts itself active
-    if (blockIdx.x == 0 && threadIdx.x < 2) atomicExch(P.queue_next + (GS_NIDLE + threadIdx.x) * QSTRIDE, 0u);
-    if ((threadIdx.x & 63) == 0) atomicAdd(P.queue + GS_ACTIVE * QSTRIDE, 1u);
+    // the next launch's counters start at zero; every wave of this launch
+    // counts itself active
+    if (blockIdx.x == 0 && threadIdx.x < 3)
+      atomicExch(reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * (1 - P.gset) + 512 * threadIdx.x), 0u);
+    if ((threadIdx.x & 63) == 0) atomicAdd(g_active, 1u);
   }
+  // (device-wide sharing) this wave's view of the board, refreshed every 4th
+  // round (every round while it is a helper): idle helper lanes, ring head /
+  // tail; whether it stays as a helper after draining
+  int gs_nid = 0;
+  uint64_t gs_h = 0, gs_t = 0;
+  bool gs_helper = false;
   if constexpr (LDS) {
     const int n16 = P.blob_bytes / 16;
     for (int i = threadIdx.x; i < n16; i += WG)
@@ -2407,14 +2434,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     if (RT_SHARE == 1 && !sh_live && !exhausted && (guard_iters & 3u) == 0u)
       sh_live = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&Bd->nidle, __ATOMIC_RELAXED, RT_WG_SCOPE)) > 0;
     if (RT_SHARE == 2 && !sh_live && !exhausted && (guard_iters & 7u) == 0u)
-      sh_live = __builtin_amdgcn_readfirstlane(lane == 0 ? (int)gs_ld32(P.queue + GS_NIDLE * QSTRIDE) : 0) > 0;
+      sh_live = __builtin_amdgcn_readfirstlane(lane == 0 ? (int)gs_ld32(g_nidle) : 0) > 0;
     if (RT_SHARE && !sh_live && exhausted) sh_live = true;
     if (RT_SHARE && !sh_live) {
       // steady state: the refill left no lane idle (else the queue is drained)
     } else if constexpr (RT_SHARE == 2) {
       // ---- device-wide work sharing (see gs_*) ----
-      unsigned int* g_nidle = P.queue + GS_NIDLE * QSTRIDE;
-      unsigned int* g_active = P.queue + GS_ACTIVE * QSTRIDE;
       auto rfl64 = [](uint64_t v) {
         return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
                (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
@@ -2424,17 +2449,28 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if (__builtin_expect(wave_any(state == S_WAIT), 0)) {
         if (state == S_WAIT && gs_done(P.gboard, wait_slot())) state = S_RESUME;
       }
-      // the launch's idle helper lanes and posted, unclaimed tickets
-      int nid = 0;
-      uint64_t gh = 0, gt = 0;
-      if (lane == 0) {
-        nid = (int)gs_ld32(g_nidle);
-        gh = gs_ld(P.gctl + GS_HEAD);
-        gt = gs_ld(P.gctl + GS_TAIL);
+      // the launch's idle helper lanes and posted, unclaimed tickets: a busy
+      // wave reads them every 4th round; a helper polls the tail every round
+      // and the others when it moved, or every 8th round
+      if (gs_helper || (guard_iters & (unsigned)RT_GS_POLL) == 0u) {
+        int nid = 0;
+        uint64_t gh = 0, gt = 0;
+        if (lane == 0) {
+          gt = gs_ld(P.gctl + GS_TAIL);
+          if (!gs_helper || (guard_iters & 7u) == 0u || gt != gs_t) {
+            nid = (int)gs_ld32(g_nidle);
+            gh = gs_ld(P.gctl + GS_HEAD);
+          } else {
+            nid = gs_nid;
+            gh = gs_h;
+          }
+        }
+        gs_nid = __builtin_amdgcn_readfirstlane(nid);
+        gs_h = rfl64(gh);
+        gs_t = rfl64(gt);
       }
-      nid = __builtin_amdgcn_readfirstlane(nid);
-      gh = rfl64(gh);
-      gt = rfl64(gt);
+      const int nid = gs_nid;
+      const uint64_t gh = gs_h, gt = gs_t;
       const long long outstanding = (long long)(gt - gh);
       // (b) owners post the pending refraction child of their shallowest
       // binary frame (frames above a claimed subtree's sentinel only) while
@@ -2443,8 +2479,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       if (__builtin_expect(want > 0 && outstanding < GS_RING / 2, 0)) {
         const bool busy_lane = state == S_TRACE || state == S_SHADE || state == S_WAIT;
         int L = -1;
+        // (a child at level L + 1 roots at most 2^(depth - L - 1) - 1 rays:
+        // only subtrees of RT_GS_MIN_LEVELS levels or more are worth a hand-off)
         if (busy_lane)
-          for (int l = sp - 1; l >= 0; l--) {
+          for (int l = min(sp - 1, P.depth - 1 - RT_GS_MIN_LEVELS); l >= 0; l--) {
             const int f = (int)(__double_as_longlong(core_ld(l, 4)) & 0xff);
             if (f & FL_TASK) break;
             if ((f & (FL_HASR | FL_HAST | FL_STAGE | FL_FORKED)) == (FL_HASR | FL_HAST)) L = l;
@@ -2552,11 +2590,22 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         my_active = busy;
       }
       if (__builtin_expect(!busy, 0)) {
-        // drained: stay while the launch may still post work; leave once no
-        // wave is busy -- a posted or claimed subtree's owner is busy until it
-        // has the colour, so then nothing is left to take (stale tickets of
+        // drained: the first RT_GS_HELPERS such waves stay while the launch
+        // may still post work, the others leave at once (thousands of pollers
+        // would saturate the board's words); a helper leaves once no wave is
+        // busy -- a posted or claimed subtree's owner is busy until it has
+        // the colour, so then nothing is left to take (stale tickets of
         // reclaimed slots may remain) -- or after RT_SHARE_SPINS idle rounds
-        const int na = __builtin_amdgcn_readfirstlane(lane == 0 ? (int)gs_ld32(g_active) : 0);
+        if (!gs_helper) {
+          unsigned int old = 0;
+          if (lane == 0) old = atomicAdd(g_helpers, 1u);
+          gs_helper = __builtin_amdgcn_readfirstlane((int)old) < RT_GS_HELPERS;
+          if (!gs_helper) {
+            if (lane == 0 && my_idle) atomicAdd(g_nidle, (unsigned int)(-my_idle));
+            break;
+          }
+        }
+        const int na = (spins & 7) ? 1 : __builtin_amdgcn_readfirstlane(lane == 0 ? (int)gs_ld32(g_active) : 0);
         if (na == 0 || ++spins > RT_SHARE_SPINS) {
 #ifdef RT_PHASE_TIMING
           if (lane == 0) atomicAdd(P.stats + ST_SHDIAG + SH_SPIN, (unsigned long long)spins);

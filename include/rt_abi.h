@@ -375,7 +375,8 @@ int rt_set_frames_in_flight(rt_context *ctx, int n);
  * reports whether an order is active and the estimate's wall time. */
 int rt_set_tile_order(rt_context *ctx, int enable);
 /* Work sharing at the tail of a launch (MI355X-specific; pixels and counters
- * are identical either way; default off). With enable = RT_SHARE_GROUP the context's
+ * are identical either way; default RT_SHARE_AUTO, below). With enable =
+ * RT_SHARE_GROUP the context's
  * specialised kernel (rt_set_specialize) is compiled with a per-workgroup
  * board in LDS: once the work queue is drained, a lane still tracing a pixel
  * posts the samples it has not started and the pending refraction children
@@ -386,11 +387,15 @@ int rt_set_tile_order(rt_context *ctx, int enable);
  * Applies to the current scene at once. */
 #define RT_SHARE_OFF 0
 #define RT_SHARE_GROUP 1
-/* RT_SHARE_DEVICE (ABI 5): the board is device-wide, in HBM -- an idle lane
- * of any drained wave on the device (any workgroup, any XCD) takes a posted
- * refraction subtree; drained waves stay to help until no wave of the launch
- * is busy. Subtrees only (no sample posting); pixel pairs run as quads. */
+/* RT_SHARE_DEVICE (ABI 5): the board is device-wide, in uncached HBM -- an
+ * idle lane of any drained wave on the device (any workgroup, any XCD) takes
+ * a posted refraction subtree; a few drained waves stay to help until no wave
+ * of the launch is busy. Subtrees only (no sample posting).
+ * RT_SHARE_AUTO (ABI 5, the default): RT_SHARE_DEVICE for scenes with CSG
+ * composites at depth >= 7 on launches of fewer than 16 pixels per lane (a
+ * strong-scaling share) or without frames in flight, else off. */
 #define RT_SHARE_DEVICE 2
+#define RT_SHARE_AUTO 3
 int rt_set_work_sharing(rt_context *ctx, int enable);
 /* Whether the current scene has a tile order, and the estimate's wall time
  * (ms) at scene setup. */

@@ -13,3 +13,7 @@ for sh in 0 2; do
 import json; d=json.load(open('$O/inflight_c4csg_share$sh.json'))
 print('share=$sh', {k: v for k, v in d.items() if k.endswith('_ms') or 'eff' in k})"
 done
+# diagnostic build: the board's event counts on rank 0's 8-rank share
+RT_AMD_LIB=build_variants/librtamd_phase.so RT_SPEC_EXTRA_FLAGS="-DRT_PHASE_TIMING" INFLIGHT_SHARE=2 INFLIGHT_F=1 INFLIGHT_WORLDS=8 INFLIGHT_RANKS=0 \
+  timeout -k 10 300 python3 scripts/inflight_emul.py c4csg 2 > $O/diag_share2.json 2> $O/diag_share2.err || { tail -5 $O/diag_share2.err; exit 1; }
+grep -E "share|waves|tail" $O/diag_share2.err | tail -4

@@ -6,7 +6,7 @@ leaves idle. F = 1 is the serial baseline (one context, one stream).
 w<N>_f<F>_eff_max = t(1 rank, F) / (N * slowest rank's share time at F): the
 efficiency the driver's 1/2/4/8-GPU bench lines give (every line runs F).
 usage: python scripts/inflight_emul.py [config] [steps]
-       (INFLIGHT_WORLDS=1,8  INFLIGHT_F=1,2,3  INFLIGHT_RANKS=all|0  INFLIGHT_SHARE=0|1|2  INFLIGHT_HINT=1|0:
+       (INFLIGHT_WORLDS=1,8  INFLIGHT_F=1,2,3  INFLIGHT_RANKS=all|0  INFLIGHT_SHARE=0|1|2  INFLIGHT_SCHED=pixel|quads|pairs  INFLIGHT_HINT=1|0:
         rt_set_frames_in_flight(F) on the contexts, as bench.py does)"""
 import json
 import os
@@ -32,12 +32,16 @@ def main():
     ctxs = []
     for _ in range(max(fs)):
         c = pkg.RenderContext(0, specialize=True)
-        if os.environ.get("INFLIGHT_SHARE", "0") != "0":  # work sharing compiled into the kernel: 1 group, 2 device
+        if os.environ.get("INFLIGHT_SHARE", "auto") != "auto":  # 0 off, 1 group, 2 device, 3 auto (default)
             c.set_work_sharing(int(os.environ["INFLIGHT_SHARE"]))
+        sched = os.environ.get("INFLIGHT_SCHED")  # pixel / quads / pairs (default: auto)
+        if sched:
+            c.set_schedule({"pixel": pkg.abi.RT_SCHED_PIXEL, "quads": pkg.abi.RT_SCHED_QUADS,
+                            "pairs": pkg.abi.RT_SCHED_PAIRS}[sched])
         c.set_scene(packed)
         ctxs.append(c)
     streams = [torch.cuda.Stream(dev) for _ in ctxs]
-    out = {"config": cfg, "steps": steps, "work_sharing": int(os.environ.get("INFLIGHT_SHARE", "0"))}
+    out = {"config": cfg, "steps": steps, "work_sharing": os.environ.get("INFLIGHT_SHARE", "auto")}
 
     def wall_ms(F, rank, world):
         drs = [pkg.dist.DistributedRenderer(ctxs[i], packed, rank, world, dev, mode="interleaved")

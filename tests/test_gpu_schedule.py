@@ -23,6 +23,7 @@ def ctxs():
     assert torch.cuda.is_available()
     g = rt.RenderContext(0)
     s = rt.RenderContext(0, specialize=True)
+    s.set_work_sharing(rt.abi.RT_SHARE_OFF)  # (the default, RT_SHARE_AUTO, shares CSG scenes)
     w = rt.RenderContext(0, specialize=True)
     w.set_work_sharing(rt.abi.RT_SHARE_GROUP)
     d = rt.RenderContext(0, specialize=True)
@@ -218,6 +219,7 @@ def test_device_sharing_full_c4csg_frame_and_shares():
     a = rt.RenderContext(0, specialize=True)
     b = rt.RenderContext(0, specialize=True)
     try:
+        a.set_work_sharing(rt.abi.RT_SHARE_OFF)
         b.set_work_sharing(rt.abi.RT_SHARE_DEVICE)
         for c in (a, b):
             c.set_scene(packed)
