@@ -259,7 +259,7 @@ struct DevScene {
   int light_mask = 0;  // bit k: the scene has lights of kind k (RT_LIGHT_*)
   bool branching = false;  // some material is reflective and transparent, or a surface program may make one
   int leaf_kind_mask = 0;  // bit k: some CSG leaf has kind k
-  size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0, off_arec = 0;
+  size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0, off_arec = 0, off_urec = 0;
   double bvh_lo[3] = {0, 0, 0}, bvh_hi[3] = {0, 0, 0};  // padded box of the BVH objects (far_shift)
   int nruns = 0;
 };
@@ -1638,10 +1638,25 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     // loops over global linear scenes: first, count, kind, axis), spheres split
     // further into scale + translation runs (axis = 1: their compact records
     // AXIS_REC doubles each, m0 m3 m5 m7 m10 m11, at off_arec by object index)
+    // and of those the runs of one uniform scale (axis = 2: m0 == m5 == m10,
+    // equal over the run; records m3 m7 m11 m0 at off_urec, rt_render.h UNI_REC)
     std::vector<int> runs;
-    std::vector<double> arec;
+    std::vector<double> arec, urec;
+    double run_scale = 0.0;
     for (int i = 0; i < s.nobj; i++) {
-      const int ax = kind[i] == RT_SPHERE && axis_sphere(&geo[(size_t)i * GEO]) ? 1 : 0;
+      int ax = kind[i] == RT_SPHERE && axis_sphere(&geo[(size_t)i * GEO]) ? 1 : 0;
+      if (ax) {
+        const double* m = &geo[(size_t)i * GEO];
+        if (m[0] == m[5] && m[0] == m[10]) {
+          ax = 2;
+          if (urec.empty()) urec.assign((size_t)s.nobj * UNI_REC, 0.0);
+          double* u = &urec[(size_t)i * UNI_REC];
+          u[0] = m[3];
+          u[1] = m[7];
+          u[2] = m[11];
+          u[3] = m[0];
+        }
+      }
       if (ax && arec.empty()) arec.assign((size_t)s.nobj * AXIS_REC, 0.0);
       if (ax) {
         const double* m = &geo[(size_t)i * GEO];
@@ -1653,16 +1668,21 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
         a[4] = m[10];
         a[5] = m[11];
       }
-      if (runs.empty() || runs[runs.size() - 2] != kind[i] || runs[runs.size() - 1] != ax)
+      const double sc = ax == 2 ? geo[(size_t)i * GEO] : 0.0;
+      if (runs.empty() || runs[runs.size() - 2] != kind[i] || runs[runs.size() - 1] != ax ||
+          (ax == 2 && sc != run_scale))
         runs.insert(runs.end(), {i, 0, kind[i], ax});
+      run_scale = sc;
       runs[runs.size() - 3]++;
     }
     s.nruns = (int)runs.size() / 4;
     s.off_runs = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
     s.off_arec = (s.off_runs + std::max<size_t>(1, runs.size()) * sizeof(int) + 63) & ~(size_t)63;
-    std::vector<char> acc(s.off_arec + std::max<size_t>(1, arec.size()) * sizeof(double), 0);
+    s.off_urec = (s.off_arec + std::max<size_t>(1, arec.size()) * sizeof(double) + 63) & ~(size_t)63;
+    std::vector<char> acc(s.off_urec + std::max<size_t>(1, urec.size()) * sizeof(double), 0);
     if (!runs.empty()) std::memcpy(acc.data() + s.off_runs, runs.data(), runs.size() * sizeof(int));
     if (!arec.empty()) std::memcpy(acc.data() + s.off_arec, arec.data(), arec.size() * sizeof(double));
+    if (!urec.empty()) std::memcpy(acc.data() + s.off_urec, urec.data(), urec.size() * sizeof(double));
     if (!b.nodes.empty()) std::memcpy(acc.data() + s.off_nodes, b.nodes.data(), b.nodes.size() * sizeof(float));
     if (s.use_bvh && !b.nodes.empty()) {
       // the box of the BVH objects' padded bounding spheres, and a generous
@@ -1981,6 +2001,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   P.runs = reinterpret_cast<const int*>(s.accel + s.off_runs);
   P.nruns = s.nruns;
   P.arec = reinterpret_cast<const double*>(s.accel + s.off_arec);
+  P.urec = reinterpret_cast<const double*>(s.accel + s.off_urec);
   if (s.use_bvh) {
     P.bvh_nodes = reinterpret_cast<const float*>(s.accel + s.off_nodes);
     P.bvh_geo = reinterpret_cast<const double*>(s.accel + s.off_bobj);

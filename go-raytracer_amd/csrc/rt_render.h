@@ -244,6 +244,7 @@ struct Params {
   const int* runs;
   int nruns;
   const double* arec;  // [nobj][AXIS_REC] compact records of axis-aligned spheres (runs with axis = 1)
+  const double* urec;  // [nobj][UNI_REC] uniform-scale spheres: m3 m7 m11 m0 (runs with axis = 2)
   int cnt_off;    // LDS byte offset of the event counters (CNT_BYTES)
   int kind_mask;  // bit k: the scene has objects of kind k
   int board_off;  // LDS byte offset of the work-sharing board (RT_SHARE == 1)
@@ -345,7 +346,16 @@ struct RecN {
 };
 typedef RecN<12> Rec12;  // WorldToObject rows (geo records, GEO doubles apart)
 typedef RecN<6> Rec6;    // axis-aligned sphere: m0 m3 m5 m7 m10 m11 (arec, AXIS_REC doubles apart)
-enum { AXIS_REC = 8 };
+typedef RecN<3> Rec3;    // uniform-scale sphere of a run: m3 m7 m11 (urec, UNI_REC doubles apart)
+enum { AXIS_REC = 8, UNI_REC = 4 };
+// Uniform-scale sphere runs (runs with axis = 2; host: m0 == m5 == m10, the
+// same value for every sphere of the run -- C5's spheres are all uscale 0.04):
+// axis_o / axis_d with a[0] = a[2] = a[4] = s make the object-space direction
+// s*d and a = dot(s*d, s*d) the same for every sphere of the run, and the
+// origin's products s*o too, so a run forms them once per ray and a sphere
+// costs o' = (s*o) + t (3 adds, bit-identical to axis_o's s*o + t) plus the
+// quadratic's c, halfB and discriminant: 17 FP64 operations instead of 28, and
+// a 24-B record instead of 48.
 template <int N, typename PT>
 __device__ __forceinline__ RecN<N> ld_rec(PT p) {
   RecN<N> r;
@@ -2884,7 +2894,29 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const bool rax = wave_all(!tr || (axis_o_ok(ray.o) && axis_d_ok(ray.d)));
           for (int r = 0; r < P.nruns; r++) {
             const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && rax) {
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] == 2 && rax) {
+              // uniform scale s for the whole run (see UNI_REC)
+              const double sc = ((cdptr)P.urec)[(size_t)r0 * UNI_REC + 3];
+              const d3 so = mk(sc * ray.o.x, sc * ray.o.y, sc * ray.o.z);
+              Ray l;
+              l.d = mk(sc * ray.d.x, sc * ray.d.y, sc * ray.d.z);
+              const double a = dot(l.d, l.d);
+              scan_records<0, 3, UNI_REC>((cdptr)P.urec, r0, rn, [&](int i, const Rec3& R) {
+                l.o = mk(so.x + R.m[0], so.y + R.m[1], so.z + R.m[2]);
+                const double hb = dot(l.o, l.d);
+                const double c = dot(l.o, l.o) - 1.0;
+                const double disc = hb * hb - a * c;
+                if (tr && !(disc < 0.0)) {
+                  const double t0 = (-hb - gsqrt(disc)) / a;
+                  if (t0 > 0.0 && (!found || t0 < best_t)) {
+                    found = true;
+                    best_t = t0;
+                    best_i = i;
+                    best_f = 0;
+                  }
+                }
+              }, [] { return false; });
+            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && rax) {
               scan_records<0, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
                 Ray l;
                 l.o = axis_o(R.m, ray.o);
@@ -3284,7 +3316,36 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       for (int r = 0; r < P.nruns; r++) {
         if (!refresh()) break;
         const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-        if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
+        if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] == 2 && sax) {
+          // uniform scale s for the run (see UNI_REC): every light's s*d and
+          // a = dot(s*d, s*d) once per run, the origin's s*o once
+          const double sc = ((cdptr)P.urec)[(size_t)r0 * UNI_REC + 3];
+          const d3 so = mk(sc * sorig.x, sc * sorig.y, sc * sorig.z);
+          d3 uld[RT_SPEC_NLIGHTS];
+          double ua[RT_SPEC_NLIGHTS];
+#pragma unroll
+          for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+            uld[li] = mk(sc * ldir_a[li].x, sc * ldir_a[li].y, sc * ldir_a[li].z);
+            ua[li] = dot(uld[li], uld[li]);
+          }
+          scan_records<RT_SHADOW_CHECK, 3, UNI_REC>((cdptr)P.urec, r0, rn, [&](int i, const Rec3& R) {
+            const d3 lo = mk(so.x + R.m[0], so.y + R.m[1], so.z + R.m[2]);
+            const double c = dot(lo, lo) - 1.0;
+#pragma unroll
+            for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
+              if (!lon[li]) continue;
+              const double hb = dot(lo, uld[li]);
+              const double disc = hb * hb - ua[li] * c;
+              if (jopen[li] && i != hit_i && !(disc < 0.0)) {
+                const double t0 = (-hb - gsqrt(disc)) / ua[li];
+                if (t0 > 0.0 && t0 * rlen < dist_a[li]) {
+                  jopen[li] = false;
+                  jsend[li] = i + 1;
+                }
+              }
+            }
+          }, [&] { return !refresh(); });
+        } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
           scan_records<RT_SHADOW_CHECK, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
             jsphere(i, axis_o(R.m, sorig), [&](int li) { return axis_d(R.m, ldir_a[li]); });
           }, [&] { return !refresh(); });
@@ -3492,7 +3553,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           for (int r = 0; r < P.nruns; r++) {
             if (!wave_any(open)) break;
             const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] == 2 && sax) {
+              const double sc = ((cdptr)P.urec)[(size_t)r0 * UNI_REC + 3];  // (see UNI_REC)
+              const d3 so = mk(sc * sr.o.x, sc * sr.o.y, sc * sr.o.z);
+              Ray l;
+              l.d = mk(sc * sr.d.x, sc * sr.d.y, sc * sr.d.z);
+              scan_records<RT_SHADOW_CHECK, 3, UNI_REC>((cdptr)P.urec, r0, rn, [&](int i, const Rec3& R) {
+                l.o = mk(so.x + R.m[0], so.y + R.m[1], so.z + R.m[2]);
+                ssphere(i, l);
+              }, [&] { return !wave_any(open); });
+            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
               scan_records<RT_SHADOW_CHECK, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
                 Ray l;
                 l.o = axis_o(R.m, sr.o);

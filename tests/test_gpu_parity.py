@@ -703,7 +703,8 @@ def test_streamed_brute_force_c5_band_matches_oracle(ctx, spec_ctx):
 
 def _axis_scene(seed, n, width, height, depth=6):
     """Spheres whose WorldToObject is a scale + translation (the diagonal
-    transform of the brute-force sphere runs, rt_render.h axis_o) in runs
+    transform of the brute-force sphere runs, rt_render.h axis_o; uniform
+    scales shared by a run: UNI_REC) in runs
     interleaved with rotated spheres, spheres with a zero translation
     component (full form: the diagonal form needs m3, m7, m11 != 0),
     non-uniform scales, exact-tie duplicates, reflective and glass materials,
@@ -720,7 +721,9 @@ def _axis_scene(seed, n, width, height, depth=6):
         r = 0.1 + 0.25 * rng.random()
         mode = (i // 9) % 4  # runs of 9 of one form
         if mode == 0:
-            o = S.Sphere(m).uscale(r).translate(x, y, z)
+            # one uniform scale per run (the brute-force loops' uniform-scale
+            # runs, rt_render.h UNI_REC; a new scale starts a new run)
+            o = S.Sphere(m).uscale(0.1 + 0.05 * ((i // 36) % 3)).translate(x, y, z)
         elif mode == 1:
             o = S.Sphere(m).scale(r, 1.5 * r, 0.7 * r).translate(x, y, z)
         elif mode == 2:
