@@ -1679,6 +1679,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     s.off_runs = s.off_planes + ((std::max<size_t>(1, planes.size()) * sizeof(int) + 15) & ~(size_t)15);
     s.off_arec = (s.off_runs + std::max<size_t>(1, runs.size()) * sizeof(int) + 63) & ~(size_t)63;
     s.off_urec = (s.off_arec + std::max<size_t>(1, arec.size()) * sizeof(double) + 63) & ~(size_t)63;
+    if (!urec.empty()) urec.resize(urec.size() + 8 * UNI_REC, 0.0);  // scan_uni may load records past a run
     std::vector<char> acc(s.off_urec + std::max<size_t>(1, urec.size()) * sizeof(double), 0);
     if (!runs.empty()) std::memcpy(acc.data() + s.off_runs, runs.data(), runs.size() * sizeof(int));
     if (!arec.empty()) std::memcpy(acc.data() + s.off_arec, arec.data(), arec.size() * sizeof(double));

@@ -442,6 +442,47 @@ __device__ __forceinline__ void scan_records(cdptr base, int r0, int rn, Body&& 
   }
 }
 
+// body(i, tx, ty, tz) for the uniform-scale spheres i = r0 .. r0 + rn - 1 in
+// index order (urec records, UNI_REC doubles: the translations m3 m7 m11):
+// two records per scalar load (one s_load_dwordx16 of 64 B), two pairs in
+// flight as in scan_records -- four spheres tested per wait instead of one,
+// so the record latency hides behind more FP64 work (brute-force C5 band
+// 1.85 -> 1.55 s). Loads may read up to 2G - 1 records past the run (the host
+// pads urec); only indices < r0 + rn reach the body. stop() (wave-uniform) is
+// asked every CHECK objects (a multiple of 2G).
+#ifndef RT_UNI_PAIRS
+#define RT_UNI_PAIRS 1
+#endif
+template <int CHECK, typename Body, typename Stop>
+__device__ __forceinline__ void scan_uni(cdptr base, int r0, int rn, Body&& body, Stop&& stop) {
+  // G records per load group (RT_UNI_PAIRS = 1: pairs, 2: quads), two groups
+  // in flight
+  constexpr int G = RT_UNI_PAIRS >= 2 ? 4 : 2, ND = G * UNI_REC;
+  static_assert(UNI_REC == 4 && CHECK % (2 * G) == 0, "scan_uni: 4-double records, stop() at group boundaries");
+  cdptr p = base + (size_t)r0 * UNI_REC;
+  RecN<ND> A = ld_rec<ND>(p);  // records j .. j + G - 1
+  int j = 0;
+  for (; j + 2 * G <= rn; j += 2 * G, p += 2 * ND) {
+    if (CHECK > 0 && j > 0 && (j % CHECK) == 0 && stop()) return;
+    const RecN<ND> B = ld_rec<ND>(after_rec(p + ND, A));  // records j + G .. j + 2G - 1
+#pragma unroll
+    for (int q = 0; q < G; q++) body(r0 + j + q, A.m[UNI_REC * q], A.m[UNI_REC * q + 1], A.m[UNI_REC * q + 2]);
+    A = ld_rec<ND>(after_rec(p + 2 * ND, B));
+#pragma unroll
+    for (int q = 0; q < G; q++) body(r0 + j + G + q, B.m[UNI_REC * q], B.m[UNI_REC * q + 1], B.m[UNI_REC * q + 2]);
+  }
+  if (j < rn) {
+    if (CHECK > 0 && j > 0 && (j % CHECK) == 0 && stop()) return;
+    const RecN<ND> B = ld_rec<ND>(after_rec(p + ND, A));
+#pragma unroll
+    for (int q = 0; q < G; q++)
+      if (j + q < rn) body(r0 + j + q, A.m[UNI_REC * q], A.m[UNI_REC * q + 1], A.m[UNI_REC * q + 2]);
+#pragma unroll
+    for (int q = 0; q < G - 1; q++)
+      if (j + G + q < rn) body(r0 + j + G + q, B.m[UNI_REC * q], B.m[UNI_REC * q + 1], B.m[UNI_REC * q + 2]);
+  }
+}
+
 // True when q = num/den (den != 0, finite) is certainly <= 0, i.e. num == 0
 // or the signs differ, so the reference would reject t = q (t <= 0) and the
 // division can be skipped. NaN operands return false (the division runs and
@@ -2901,8 +2942,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               Ray l;
               l.d = mk(sc * ray.d.x, sc * ray.d.y, sc * ray.d.z);
               const double a = dot(l.d, l.d);
-              scan_records<0, 3, UNI_REC>((cdptr)P.urec, r0, rn, [&](int i, const Rec3& R) {
-                l.o = mk(so.x + R.m[0], so.y + R.m[1], so.z + R.m[2]);
+              auto ubody = [&](int i, double tx, double ty, double tz) {
+                l.o = mk(so.x + tx, so.y + ty, so.z + tz);
                 const double hb = dot(l.o, l.d);
                 const double c = dot(l.o, l.o) - 1.0;
                 const double disc = hb * hb - a * c;
@@ -2915,7 +2956,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                     best_f = 0;
                   }
                 }
-              }, [] { return false; });
+              };
+              if (RT_UNI_PAIRS)
+                scan_uni<0>((cdptr)P.urec, r0, rn, ubody, [] { return false; });
+              else
+                scan_records<0, 3, UNI_REC>((cdptr)P.urec, r0, rn, [&](int i, const Rec3& R) { ubody(i, R.m[0], R.m[1], R.m[2]); },
+                                            [] { return false; });
             } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && rax) {
               scan_records<0, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
                 Ray l;
@@ -3328,8 +3374,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             uld[li] = mk(sc * ldir_a[li].x, sc * ldir_a[li].y, sc * ldir_a[li].z);
             ua[li] = dot(uld[li], uld[li]);
           }
-          scan_records<RT_SHADOW_CHECK, 3, UNI_REC>((cdptr)P.urec, r0, rn, [&](int i, const Rec3& R) {
-            const d3 lo = mk(so.x + R.m[0], so.y + R.m[1], so.z + R.m[2]);
+          auto ubody = [&](int i, double tx, double ty, double tz) {
+            const d3 lo = mk(so.x + tx, so.y + ty, so.z + tz);
             const double c = dot(lo, lo) - 1.0;
 #pragma unroll
             for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
@@ -3344,7 +3390,13 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                 }
               }
             }
-          }, [&] { return !refresh(); });
+          };
+          if (RT_UNI_PAIRS)
+            scan_uni<RT_SHADOW_CHECK>((cdptr)P.urec, r0, rn, ubody, [&] { return !refresh(); });
+          else
+            scan_records<RT_SHADOW_CHECK, 3, UNI_REC>((cdptr)P.urec, r0, rn,
+                                                      [&](int i, const Rec3& R) { ubody(i, R.m[0], R.m[1], R.m[2]); },
+                                                      [&] { return !refresh(); });
         } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
           scan_records<RT_SHADOW_CHECK, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
             jsphere(i, axis_o(R.m, sorig), [&](int li) { return axis_d(R.m, ldir_a[li]); });
