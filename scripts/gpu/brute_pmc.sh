@@ -2,7 +2,7 @@
 # row band of BASELINE config 5 (7680x4320, 100k spheres): bench line,
 # rocprofv3 kernel stats, PMC passes (instruction mix, FP64 counts, waits) and
 # the diagnostic build's lane-utilisation counters.
-# usage: bash scripts/gpu_brute_pmc.sh TAG [ROWS]     (ROWS default 2048:2304: ~10 pixels per lane, so the tail stays short)
+# usage: bash scripts/gpu/brute_pmc.sh TAG [ROWS]     (ROWS default 2048:2304: ~10 pixels per lane, so the tail stays short)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-c5band}

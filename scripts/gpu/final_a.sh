@@ -1,12 +1,12 @@
-# Round-4 evidence, part A: PMC passes for every bench config (copied into
+# Round-5 evidence, part A: PMC passes for every bench config (copied into
 # profiles/ on the box so the bench lines quote them), the default bench line,
 # its rocprofv3 kernel-trace summary, and smoke().
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=${O:-gpurun_out/final_r4}
+O=${O:-gpurun_out/final_r5}
 mkdir -p $O
-bash scripts/gpu_pmc_all.sh "${PMC_CFGS:-c3 c3cone c4 c4csg c5}" > $O/pmc_all.log 2>&1 || { tail -5 $O/pmc_all.log; exit 1; }
+bash scripts/gpu/pmc_all.sh "${PMC_CFGS:-c3 c3cone c4 c4csg c5}" > $O/pmc_all.log 2>&1 || { tail -5 $O/pmc_all.log; exit 1; }
 for c in ${PMC_CFGS:-c3 c3cone c4 c4csg c5}; do
   cp gpurun_out/pmc_$c/pmc_$c.json profiles/pmc_$c.json && cp gpurun_out/pmc_$c/traffic.json profiles/traffic_$c.json || exit 1
 done

@@ -1,9 +1,9 @@
-# Round-4 evidence, part B: every config's bench line with its CPU baseline,
+# Round-5 evidence, part B: every config's bench line with its CPU baseline,
 # and the GPU test suite.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=${O:-gpurun_out/final_r4}
+O=${O:-gpurun_out/final_r5}
 mkdir -p $O/sweep
 for c in ${SWEEP_CFGS:-c1 c2 canned c3 c3cone c4 c4csg c5}; do
   steps=10; [ $c = c5 ] && steps=3; [ $c = c4csg ] && steps=5

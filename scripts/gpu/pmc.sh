@@ -1,6 +1,6 @@
 # PMC passes for the bench kernel (one rocprofv3 run per counter group), plus
 # the FETCH_SIZE / WRITE_SIZE calibration for the kernel's access widths.
-# usage: bash scripts/gpu_pmc.sh [config]   (default c3)
+# usage: bash scripts/gpu/pmc.sh [config]   (default c3)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 CFG=${1:-c3}

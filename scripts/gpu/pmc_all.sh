@@ -1,12 +1,12 @@
-# PMC passes (scripts/gpu_pmc.sh) for every BASELINE config the bench quotes:
+# PMC passes (scripts/gpu/pmc.sh) for every BASELINE config the bench quotes:
 # profiles/pmc_<cfg>.json (executed FP64 work, issue / lane utilisation) and
 # profiles/traffic_<cfg>.json (calibrated HBM bytes) land under gpurun_out/pmc_<cfg>/.
-# usage: bash scripts/gpu_pmc_all.sh "c3 c3cone c4 c4csg c5"
+# usage: bash scripts/gpu/pmc_all.sh "c3 c3cone c4 c4csg c5"
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for c in ${1:-c3 c3cone c4 c4csg c5}; do
   # the schedule the in-flight bench picks (C4 whole frames: pixel pairs), one dispatch at a time
   args=""; [ $c = c4 ] && args="--schedule pairs"
-  PMC_BENCH_ARGS="$args" bash scripts/gpu_pmc.sh $c > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 gpurun_out/pmc_$c.log; exit 1; }
+  PMC_BENCH_ARGS="$args" bash scripts/gpu/pmc.sh $c > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 gpurun_out/pmc_$c.log; exit 1; }
   echo "== $c"; tail -2 gpurun_out/pmc_$c.log
 done
