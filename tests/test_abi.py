@@ -60,3 +60,18 @@ def test_render_without_device_fails_loudly():
         pytest.skip("a HIP device is present")
     with pytest.raises(rt.render.RenderError):
         rt.Render(rt.configs.c1(width=8, height=8))
+
+
+def test_python_constants_mirror_the_header():
+    """Every integer #define of include/rt_abi.h that the ctypes mirror also
+    names (kinds, status codes, schedules, work-sharing modes, info bits...)
+    has the header's value."""
+    src = open(HEADER).read()
+    defs = {m.group(1): int(m.group(2)) for m in re.finditer(r"^#define\s+(RT_\w+)\s+\(?(-?\d+)\)?\s*(?:/\*.*)?$", src, re.M)}
+    a = rt.abi
+    checked = [n for n in defs if hasattr(a, n)]
+    for n in checked:
+        assert getattr(a, n) == defs[n], n
+    for n in ["RT_SHARE_OFF", "RT_SHARE_GROUP", "RT_SHARE_DEVICE", "RT_SHARE_AUTO", "RT_INFO_SHARE_DEVICE",
+              "RT_ABI_VERSION", "RT_SCHED_PAIRS", "RT_CSG"]:
+        assert n in checked, n
