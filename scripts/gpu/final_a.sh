@@ -15,5 +15,16 @@ timeout -k 10 600 python3 bench.py > $O/bench_default.json 2> $O/bench_default.e
 cat $O/bench_default.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof -o c3 --output-format csv -- python3 bench.py --steps 30 --warmup 3 --cpu-baseline off --companion off > $O/rocprof_bench.json 2> $O/rocprof_bench.err || { tail -5 $O/rocprof_bench.err; exit 1; }
 python3 scripts/trace_span.py "$(find $O/rocprof -name '*kernel_trace.csv' | head -1)" 30 $O/trace_span_c3.json
+# the same run's HIP-event span (its bench line) and rocprofv3 trace span, side by side
+python3 - "$O" <<'PY'
+import json, sys
+O = sys.argv[1]
+line = json.loads(open(O + "/rocprof_bench.json").read().strip().splitlines()[-1])
+ts = json.load(open(O + "/trace_span_c3.json"))
+line["roofline"]["trace_span_ms"] = round(ts["span_ms_per_frame"], 4)
+line["roofline"]["trace_span_source"] = "rocprofv3 --kernel-trace of this run (scripts/trace_span.py)"
+json.dump(line, open(O + "/bench_c3_rocprof_spans.json", "w"))
+print("event span", line["roofline"]["kernel_ms"], "trace span", line["roofline"]["trace_span_ms"])
+PY
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
 tail -2 $O/smoke.log
