@@ -453,6 +453,17 @@ __device__ __forceinline__ void scan_records(cdptr base, int r0, int rn, Body&& 
 #ifndef RT_UNI_PAIRS
 #define RT_UNI_PAIRS 1
 #endif
+// after_rec for scan_uni's 16-dword groups: the dependency goes through a
+// readfirstlane of the record's first dword. Under SGPR pressure (3 lights)
+// the compiler kept a group in VGPRs, and the asm's "s" operand then needed
+// an illegal VGPR -> SGPR copy (hipRTC aborted the process); v_readfirstlane
+// is the legal copy, and it folds away when the value is in an SGPR already.
+template <int N>
+__device__ __forceinline__ cdptr after_rec_u(cdptr next, const RecN<N>& cur) {
+  const int dep = __builtin_amdgcn_readfirstlane(__double2loint(cur.m[0]));
+  asm volatile("" : "+s"(next) : "s"(dep));
+  return next;
+}
 template <int CHECK, typename Body, typename Stop>
 __device__ __forceinline__ void scan_uni(cdptr base, int r0, int rn, Body&& body, Stop&& stop) {
   // G records per load group (RT_UNI_PAIRS = 1: pairs, 2: quads), two groups
@@ -464,16 +475,16 @@ __device__ __forceinline__ void scan_uni(cdptr base, int r0, int rn, Body&& body
   int j = 0;
   for (; j + 2 * G <= rn; j += 2 * G, p += 2 * ND) {
     if (CHECK > 0 && j > 0 && (j % CHECK) == 0 && stop()) return;
-    const RecN<ND> B = ld_rec<ND>(after_rec(p + ND, A));  // records j + G .. j + 2G - 1
+    const RecN<ND> B = ld_rec<ND>(after_rec_u(p + ND, A));  // records j + G .. j + 2G - 1
 #pragma unroll
     for (int q = 0; q < G; q++) body(r0 + j + q, A.m[UNI_REC * q], A.m[UNI_REC * q + 1], A.m[UNI_REC * q + 2]);
-    A = ld_rec<ND>(after_rec(p + 2 * ND, B));
+    A = ld_rec<ND>(after_rec_u(p + 2 * ND, B));
 #pragma unroll
     for (int q = 0; q < G; q++) body(r0 + j + G + q, B.m[UNI_REC * q], B.m[UNI_REC * q + 1], B.m[UNI_REC * q + 2]);
   }
   if (j < rn) {
     if (CHECK > 0 && j > 0 && (j % CHECK) == 0 && stop()) return;
-    const RecN<ND> B = ld_rec<ND>(after_rec(p + ND, A));
+    const RecN<ND> B = ld_rec<ND>(after_rec_u(p + ND, A));
 #pragma unroll
     for (int q = 0; q < G; q++)
       if (j + q < rn) body(r0 + j + q, A.m[UNI_REC * q], A.m[UNI_REC * q + 1], A.m[UNI_REC * q + 2]);
@@ -2934,8 +2945,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           // scale + translation spheres take the diagonal transform (exact, see axis_o)
           const bool rax = wave_all(!tr || (axis_o_ok(ray.o) && axis_d_ok(ray.d)));
           for (int r = 0; r < P.nruns; r++) {
-            const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] == 2 && rax) {
+            // (wave-uniform run fields: readfirstlane keeps the record addresses in SGPRs)
+            const int r0 = __builtin_amdgcn_readfirstlane(P.runs[4 * r]), rn = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 1]),
+                      rk = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 2]), rax_k = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 3]);
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && rax_k == 2 && rax) {
               // uniform scale s for the whole run (see UNI_REC)
               const double sc = ((cdptr)P.urec)[(size_t)r0 * UNI_REC + 3];
               const d3 so = mk(sc * ray.o.x, sc * ray.o.y, sc * ray.o.z);
@@ -2962,7 +2975,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               else
                 scan_records<0, 3, UNI_REC>((cdptr)P.urec, r0, rn, [&](int i, const Rec3& R) { ubody(i, R.m[0], R.m[1], R.m[2]); },
                                             [] { return false; });
-            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && rax) {
+            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && rax_k && rax) {
               scan_records<0, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
                 Ray l;
                 l.o = axis_o(R.m, ray.o);
@@ -3303,7 +3316,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(LTP(li), ldir_a[li], dist_a[li]);
 #endif
     PH_MARK(5);
-#if RT_STREAM_SMEM && !RT_CULL && RT_SHADOW_JOINT && !defined(RT_SPEC_NOBJ)
+// (at most 4 lights: with 5-8 the joint sweep's per-light state broke the
+// backend -- "illegal VGPR to SGPR copy", which aborts the process inside
+// hipRTC -- in round 4's code as in this one; scripts/spec_matrix.sh)
+#if RT_STREAM_SMEM && !RT_CULL && RT_SHADOW_JOINT && !defined(RT_SPEC_NOBJ) && RT_SPEC_NLIGHTS <= 4
 #define RT_JOINT_SWEEP 1
 #else
 #define RT_JOINT_SWEEP 0
@@ -3324,15 +3340,16 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     }
     if constexpr (STREAM) {
       const cdptr cgeo = (cdptr)S.geo;
-      bool lon[RT_SPEC_NLIGHTS];  // wave-uniform: light li still has an open lane
+      // wave-uniform: bit li = light li still has an open lane (one scalar
+      // mask: an array of 8 such flags was kept in VGPRs and its branches then
+      // needed an illegal VGPR -> SGPR copy)
+      int lonm = 0;
       auto refresh = [&]() {
-        bool any = false;
+        int m = 0;
 #pragma unroll
-        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-          lon[li] = wave_any(jopen[li]);
-          any = any || lon[li];
-        }
-        return any;
+        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) m |= wave_any(jopen[li]) ? (1 << li) : 0;
+        lonm = __builtin_amdgcn_readfirstlane(m);
+        return lonm != 0;
       };
       // one object against every light's shadow ray: lo = the shared
       // object-space origin; ldir(li) = light li's object-space direction
@@ -3340,7 +3357,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         const double c = dot(lo, lo) - 1.0;
 #pragma unroll
         for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-          if (!lon[li]) continue;
+          if (!((lonm >> li) & 1)) continue;
           const d3 ld = ldir(li);
           const double a = dot(ld, ld);
           const double hb = dot(lo, ld);
@@ -3361,8 +3378,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       const bool sax = wave_all(sax_l);
       for (int r = 0; r < P.nruns; r++) {
         if (!refresh()) break;
-        const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-        if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] == 2 && sax) {
+        // (wave-uniform run fields: readfirstlane keeps the record addresses in SGPRs)
+            const int r0 = __builtin_amdgcn_readfirstlane(P.runs[4 * r]), rn = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 1]),
+                      rk = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 2]), rax_k = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 3]);
+        if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && rax_k == 2 && sax) {
           // uniform scale s for the run (see UNI_REC): every light's s*d and
           // a = dot(s*d, s*d) once per run, the origin's s*o once
           const double sc = ((cdptr)P.urec)[(size_t)r0 * UNI_REC + 3];
@@ -3379,7 +3398,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const double c = dot(lo, lo) - 1.0;
 #pragma unroll
             for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-              if (!lon[li]) continue;
+              if (!((lonm >> li) & 1)) continue;
               const double hb = dot(lo, uld[li]);
               const double disc = hb * hb - ua[li] * c;
               if (jopen[li] && i != hit_i && !(disc < 0.0)) {
@@ -3397,7 +3416,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             scan_records<RT_SHADOW_CHECK, 3, UNI_REC>((cdptr)P.urec, r0, rn,
                                                       [&](int i, const Rec3& R) { ubody(i, R.m[0], R.m[1], R.m[2]); },
                                                       [&] { return !refresh(); });
-        } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
+        } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && rax_k && sax) {
           scan_records<RT_SHADOW_CHECK, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
             jsphere(i, axis_o(R.m, sorig), [&](int li) { return axis_d(R.m, ldir_a[li]); });
           }, [&] { return !refresh(); });
@@ -3604,8 +3623,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const bool sax = wave_all(!hit || (axis_o_ok(sr.o) && axis_d_ok(sr.d)));
           for (int r = 0; r < P.nruns; r++) {
             if (!wave_any(open)) break;
-            const int r0 = P.runs[4 * r], rn = P.runs[4 * r + 1], rk = P.runs[4 * r + 2];
-            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] == 2 && sax) {
+            // (wave-uniform run fields: readfirstlane keeps the record addresses in SGPRs)
+            const int r0 = __builtin_amdgcn_readfirstlane(P.runs[4 * r]), rn = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 1]),
+                      rk = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 2]), rax_k = __builtin_amdgcn_readfirstlane(P.runs[4 * r + 3]);
+            if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && rax_k == 2 && sax) {
               const double sc = ((cdptr)P.urec)[(size_t)r0 * UNI_REC + 3];  // (see UNI_REC)
               const d3 so = mk(sc * sr.o.x, sc * sr.o.y, sc * sr.o.z);
               Ray l;
@@ -3614,7 +3635,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
                 l.o = mk(so.x + R.m[0], so.y + R.m[1], so.z + R.m[2]);
                 ssphere(i, l);
               }, [&] { return !wave_any(open); });
-            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && P.runs[4 * r + 3] && sax) {
+            } else if (spec_kind(RT_SPHERE) && rk == RT_SPHERE && rax_k && sax) {
               scan_records<RT_SHADOW_CHECK, 6, AXIS_REC>((cdptr)P.arec, r0, rn, [&](int i, const Rec6& R) {
                 Ray l;
                 l.o = axis_o(R.m, sr.o);
