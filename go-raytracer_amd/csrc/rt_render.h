@@ -1664,12 +1664,25 @@ __device__ __forceinline__ uint64_t low_bits(uint64_t m, int n) {
 #ifndef RT_GS_MIN_LEVELS
 #define RT_GS_MIN_LEVELS 3  // post only refraction children with >= this many levels below them
 #endif
+// Sharded by XCD (RT_GS_SHARDS rings; a workgroup posts to ring blockIdx mod
+// shards -- blocks are dealt round-robin over the 8 XCDs, so a ring's posters
+// share an L2 and a memory path; placement only affects speed): each ring
+// has its own head / tail words, and the idle-lane count is replicated per
+// shard (an update adds to every replica, one wave instruction with a lane
+// per replica), so a busy wave's poll reads words only its shard's waves read.
+#ifndef RT_GS_SHARDS
+#define RT_GS_SHARDS 8
+#endif
 enum { GS_FREE = 0, GS_POSTED = 1, GS_CLAIMED = 2, GS_DONE = 3, GS_REC = 8 /* u64 per slot */,
-       GS_RING = 1 << 20 /* ring entries (u64) */,
+       GS_RING = 1 << 20 /* ring entries (u64), all shards */, GS_SH = RT_GS_SHARDS,
+       GS_RSH = GS_RING / GS_SH /* entries per shard's ring */,
        // control block (u64 indices; the words 4 KB apart, so no two share a
-       // memory channel): ring head / tail, then two counter sets
-       GS_HEAD = 0, GS_TAIL = 512, GS_SET = 1024 /* set s at GS_SET + GS_SETSZ * s */, GS_SETSZ = 1536,
-       GS_NIDLE = 0, GS_ACTIVE = 512, GS_HELPERS = 1024 /* u64 in a set */, GS_CTL_U64 = GS_SET + 2 * GS_SETSZ };
+       // memory channel): shard k's ring head / tail at GS_SHARD * k + 0 / 512,
+       // then two counter sets: active waves, helper waves, idle lanes per shard
+       GS_SHARD = 1024, GS_HEAD = 0, GS_TAIL = 512, GS_SET = GS_SHARD * GS_SH /* set s at GS_SET + GS_SETSZ * s */,
+       GS_ACTIVE = 0, GS_HELPERS = 512, GS_NIDLE = 1024 /* + 512 * shard */, GS_SETSZ = 1024 + 512 * GS_SH,
+       GS_CTL_U64 = GS_SET + 2 * GS_SETSZ };
+static_assert(GS_SH >= 1 && GS_SH <= 32 && (GS_RING % GS_SH) == 0 && (GS_RSH & (GS_RSH - 1)) == 0, "RT_GS_SHARDS");
 #ifndef RT_GS_POLL
 #define RT_GS_POLL 15  // a busy wave reads the board's words every (RT_GS_POLL + 1)-th round
 #endif
@@ -1889,13 +1902,25 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   }
   if (blockIdx.x == 0 && threadIdx.x < QHEADS) atomicExch(P.queue_next + threadIdx.x * QSTRIDE, 0u);
   // device-wide sharing: this launch's idle-lane / active-wave counters
-  unsigned int* g_nidle = reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * P.gset + GS_NIDLE);
-  unsigned int* g_active = reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * P.gset + GS_ACTIVE);
-  unsigned int* g_helpers = reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * P.gset + GS_HELPERS);
+  // (device-wide sharing) this workgroup's shard: its ring, its replica of
+  // the idle-lane count
+  const int gshard = (int)(blockIdx.x % (unsigned)GS_SH);
+  uint64_t* const g_ring = P.gring + (size_t)gshard * GS_RSH;
+  uint64_t* const g_head = P.gctl + GS_SHARD * gshard + GS_HEAD;
+  uint64_t* const g_tail = P.gctl + GS_SHARD * gshard + GS_TAIL;
+  uint64_t* const g_set = P.gctl + GS_SET + GS_SETSZ * P.gset;
+  unsigned int* g_nidle = reinterpret_cast<unsigned int*>(g_set + GS_NIDLE + 512 * gshard);
+  unsigned int* g_active = reinterpret_cast<unsigned int*>(g_set + GS_ACTIVE);
+  unsigned int* g_helpers = reinterpret_cast<unsigned int*>(g_set + GS_HELPERS);
+  // idle-lane count updates go to every shard's replica (lane k: replica k)
+  auto nidle_add = [&](int delta) {
+    if ((int)(threadIdx.x & 63) < GS_SH)
+      atomicAdd(reinterpret_cast<unsigned int*>(g_set + GS_NIDLE + 512 * (threadIdx.x & 63)), (unsigned int)delta);
+  };
   if constexpr (RT_SHARE == 2) {
     // the next launch's counters start at zero; every wave of this launch
     // counts itself active
-    if (blockIdx.x == 0 && threadIdx.x < 3)
+    if (blockIdx.x == 0 && threadIdx.x < 2 + GS_SH)
       atomicExch(reinterpret_cast<unsigned int*>(P.gctl + GS_SET + GS_SETSZ * (1 - P.gset) + 512 * threadIdx.x), 0u);
     if ((threadIdx.x & 63) == 0) atomicAdd(g_active, 1u);
   }
@@ -2518,10 +2543,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         int nid = 0;
         uint64_t gh = 0, gt = 0;
         if (lane == 0) {
-          gt = gs_ld(P.gctl + GS_TAIL);
+          gt = gs_ld(g_tail);
           if (!gs_helper || (guard_iters & 7u) == 0u || gt != gs_t) {
             nid = (int)gs_ld32(g_nidle);
-            gh = gs_ld(P.gctl + GS_HEAD);
+            gh = gs_ld(g_head);
           } else {
             nid = gs_nid;
             gh = gs_h;
@@ -2538,7 +2563,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       // binary frame (frames above a claimed subtree's sentinel only) while
       // idle lanes anywhere on the device outnumber the posted tickets
       const int want = nid - (int)min(outstanding, (long long)(1 << 30));
-      if (__builtin_expect(want > 0 && outstanding < GS_RING / 2, 0)) {
+      if (__builtin_expect(want > 0 && outstanding < GS_RSH / 2, 0)) {
         const bool busy_lane = state == S_TRACE || state == S_SHADE || state == S_WAIT;
         int L = -1;
         // (a child at level L + 1 roots at most 2^(depth - L - 1) - 1 rays:
@@ -2576,27 +2601,50 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           }
           gs_drain();  // every posted slot's state has landed before its ticket
           uint64_t t0 = 0;
-          if (lane == 0) t0 = __hip_atomic_fetch_add(P.gctl + GS_TAIL, (uint64_t)npost, __ATOMIC_RELAXED, RT_AG_SCOPE);
+          if (lane == 0) t0 = __hip_atomic_fetch_add(g_tail, (uint64_t)npost, __ATOMIC_RELAXED, RT_AG_SCOPE);
           t0 = rfl64(t0);
           if (post) {
             const uint64_t t = t0 + (uint64_t)rk;
-            gs_st(P.gring + (t & (GS_RING - 1)), (t << 32) | (uint32_t)q);
+            gs_st(g_ring + (t & (GS_RSH - 1)), (t << 32) | (uint32_t)q);
           }
         }
       }
-      // (c) idle lanes of a drained wave claim tickets
+      // (c) idle lanes of a drained wave claim tickets: from its own shard's
+      // ring, or -- a helper whose ring is empty, every 4th round -- from the
+      // first other shard with tickets (one load per shard, a lane each)
       uint64_t il = exhausted ? wave_ballot(state == S_IDLE) : 0ull;
-      if (__builtin_expect(il != 0 && outstanding > 0 && !P.est_out, 0)) {
+      int cshard = gshard;
+      uint64_t ch = gh;
+      bool ctry = outstanding > 0;
+      if (GS_SH > 1 && il != 0 && !ctry && gs_helper && (guard_iters & 3u) == 0u && !P.est_out) {
+        const int k = lane < GS_SH ? (gshard + 1 + lane) % GS_SH : gshard;
+        uint64_t ot = 0, oh = 0;
+        if (lane < GS_SH - 1) {
+          ot = gs_ld(P.gctl + GS_SHARD * k + GS_TAIL);
+          oh = gs_ld(P.gctl + GS_SHARD * k + GS_HEAD);
+        }
+        const uint64_t hasm = wave_ballot(lane < GS_SH - 1 && ot > oh);
+        if (hasm) {
+          const int fl = __builtin_ctzll(hasm);
+          cshard = (gshard + 1 + fl) % GS_SH;
+          ch = rfl64(__shfl(oh, fl));
+          ctry = true;
+        }
+      }
+      if (__builtin_expect(il != 0 && ctry && !P.est_out, 0)) {
+        uint64_t* const c_head = P.gctl + GS_SHARD * cshard + GS_HEAD;
+        uint64_t* const c_tail = P.gctl + GS_SHARD * cshard + GS_TAIL;
+        uint64_t* const c_ring = P.gring + (size_t)cshard * GS_RSH;
         const int nil = (int)__popcll(il);
         uint64_t h = 0;
         int k = 0;
         if (lane == 0) {
-          uint64_t hh = gh;
+          uint64_t hh = ch;
           for (int tries = 0; tries < 4; tries++) {
-            const uint64_t tt = gs_ld(P.gctl + GS_TAIL);
+            const uint64_t tt = gs_ld(c_tail);
             const int kk = tt > hh ? (int)min((uint64_t)nil, tt - hh) : 0;
             if (kk <= 0) break;
-            if (__hip_atomic_compare_exchange_strong(P.gctl + GS_HEAD, &hh, hh + (uint64_t)kk, __ATOMIC_RELAXED,
+            if (__hip_atomic_compare_exchange_strong(c_head, &hh, hh + (uint64_t)kk, __ATOMIC_RELAXED,
                                                      __ATOMIC_RELAXED, RT_AG_SCOPE)) {
               h = hh;
               k = kk;
@@ -2614,7 +2662,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             uint64_t e = 0;
             // the poster writes the ticket's entry right after taking it
             for (int w_ = 0; w_ < (1 << 14); w_++) {
-              e = gs_ld(P.gring + (t & (GS_RING - 1)));
+              e = gs_ld(c_ring + (t & (GS_RSH - 1)));
               if ((uint32_t)(e >> 32) == (uint32_t)t) break;
               __builtin_amdgcn_s_sleep(1);
             }
@@ -2643,7 +2691,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       // waves still busy
       const int cur_idle = (exhausted && !P.est_out) ? (int)__popcll(il) : 0;
       if (cur_idle != my_idle) {
-        if (lane == 0) atomicAdd(g_nidle, (unsigned int)(cur_idle - my_idle));
+        nidle_add(cur_idle - my_idle);
         my_idle = cur_idle;
       }
       const bool busy = wave_any(state != S_IDLE);
@@ -2663,7 +2711,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           if (lane == 0) old = atomicAdd(g_helpers, 1u);
           gs_helper = __builtin_amdgcn_readfirstlane((int)old) < RT_GS_HELPERS;
           if (!gs_helper) {
-            if (lane == 0 && my_idle) atomicAdd(g_nidle, (unsigned int)(-my_idle));
+            if (my_idle) nidle_add(-my_idle);
             break;
           }
         }
@@ -2672,7 +2720,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 #ifdef RT_PHASE_TIMING
           if (lane == 0) atomicAdd(P.stats + ST_SHDIAG + SH_SPIN, (unsigned long long)spins);
 #endif
-          if (lane == 0 && my_idle) atomicAdd(g_nidle, (unsigned int)(-my_idle));
+          if (my_idle) nidle_add(-my_idle);
           break;
         }
         __builtin_amdgcn_s_sleep(RT_SHARE_SLEEP);
@@ -3238,6 +3286,23 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     const float rlen_rcpf = __builtin_amdgcn_rcpf((float)rlen);
 #endif
     const d3 sorig = add(pw, scale(nw, 1e-4));
+#ifndef RT_PLANE_HOIST
+#define RT_PLANE_HOIST 0  // small specialised scenes: the plane culls' origin half once per hit, not per light
+#endif
+#if defined(RT_SPEC_NOBJ) && RT_CULL && RT_PLANE_HOIST
+    // every light's shadow ray starts at sorig: a plane cull's f(0) and its
+    // term scale (may_hit_plane_o) are the same for all of them
+    PlaneO spo[RT_SPEC_NOBJ];
+    {
+      const F3 hof = f3(sorig);
+#pragma unroll
+      for (int i = 0; i < RT_SPEC_NOBJ; i++)
+        if (spec_kinds[i] == RT_PLANE) spo[i] = may_hit_plane_o(hof, SHP(i));
+    }
+#define SH_PLANE_CULL(i, d, tmax) may_hit_plane_d(spo[i], d, tmax, SHP(i))
+#else
+#define SH_PLANE_CULL(i, d, tmax) may_hit_plane(sof, d, tmax, SHP(i))
+#endif
 #ifndef RT_CULL_HOIST
 #define RT_CULL_HOIST 0  // measured: -1.5 % VALU but the live arrays spill (C3 +2 %, C2 -0.5 %)
 #endif
@@ -3700,7 +3765,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           if (!wave_any(test)) continue;
 #elif RT_CULL
           test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
-                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, SHP(i)));
+                               : CULL_AND(test, SH_PLANE_CULL(i, sdf, stmax));
           if (!wave_any(test)) continue;
 #endif
           EXDIAG(k, 1, test);
