@@ -1684,7 +1684,10 @@ enum { GS_FREE = 0, GS_POSTED = 1, GS_CLAIMED = 2, GS_DONE = 3, GS_REC = 8 /* u6
        GS_CTL_U64 = GS_SET + 2 * GS_SETSZ };
 static_assert(GS_SH >= 1 && GS_SH <= 32 && (GS_RING % GS_SH) == 0 && (GS_RSH & (GS_RSH - 1)) == 0, "RT_GS_SHARDS");
 #ifndef RT_GS_POLL
-#define RT_GS_POLL 15  // a busy wave reads the board's words every (RT_GS_POLL + 1)-th round
+// a busy wave reads the board's words every (RT_GS_POLL + 1)-th round
+// (c4csg 8-rank share, profiles/r05/gpoll: 1.77-1.79 ms at 3, 1.77-1.81 at
+// 1, 1.83 at 0, 1.95 at 15; sharded rings make frequent polls cheap)
+#define RT_GS_POLL 3
 #endif
 #ifndef RT_GS_HELPERS
 #define RT_GS_HELPERS 16  // drained waves that stay to help (device-wide); the others leave at once
@@ -3286,23 +3289,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     const float rlen_rcpf = __builtin_amdgcn_rcpf((float)rlen);
 #endif
     const d3 sorig = add(pw, scale(nw, 1e-4));
-#ifndef RT_PLANE_HOIST
-#define RT_PLANE_HOIST 0  // small specialised scenes: the plane culls' origin half once per hit, not per light
-#endif
-#if defined(RT_SPEC_NOBJ) && RT_CULL && RT_PLANE_HOIST
-    // every light's shadow ray starts at sorig: a plane cull's f(0) and its
-    // term scale (may_hit_plane_o) are the same for all of them
-    PlaneO spo[RT_SPEC_NOBJ];
-    {
-      const F3 hof = f3(sorig);
-#pragma unroll
-      for (int i = 0; i < RT_SPEC_NOBJ; i++)
-        if (spec_kinds[i] == RT_PLANE) spo[i] = may_hit_plane_o(hof, SHP(i));
-    }
-#define SH_PLANE_CULL(i, d, tmax) may_hit_plane_d(spo[i], d, tmax, SHP(i))
-#else
+// (hoisting the plane culls' origin half out of the light loop measured
+// +4.6 % on C3, profiles/r05/c3_ab: not kept)
 #define SH_PLANE_CULL(i, d, tmax) may_hit_plane(sof, d, tmax, SHP(i))
-#endif
 #ifndef RT_CULL_HOIST
 #define RT_CULL_HOIST 0  // measured: -1.5 % VALU but the live arrays spill (C3 +2 %, C2 -0.5 %)
 #endif
