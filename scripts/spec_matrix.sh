@@ -2,7 +2,9 @@
 # Offline compile of specialised kernel variants (as hipRTC builds them at run
 # time) over a matrix of scene shapes: a backend error ("illegal VGPR to SGPR
 # copy" and the like) aborts the process inside hipRTC, so catch it here.
-# usage: scripts/spec_matrix.sh [jobs]   -> prints FAIL lines, exit 1 on any failure
+# usage: [SPEC_EXTRA="<options>"] scripts/spec_matrix.sh [jobs]
+#   -> prints FAIL lines, exit 1 on any failure (SPEC_EXTRA: options added to
+#      every variant, e.g. an RT_SPEC_EXTRA_FLAGS candidate)
 R=$(cd "$(dirname "$0")/.." && pwd)
 J=${1:-6}
 cases=()
@@ -29,9 +31,10 @@ cases+=("-DRT_SPEC_KMASK=15 -DRT_SPEC_FEAT=0 -DRT_SPEC_NOBJ=4 -DRT_SPEC_KINDS=1,
 cases+=("-DRT_SPEC_KMASK=15 -DRT_SPEC_FEAT=0 -DRT_SPEC_NOBJ=4 -DRT_SPEC_KINDS=1,3,2,0 -DRT_SPEC_NLIGHTS=4 -DRT_SPEC_POWBITS=6 -DRT_PAIRS=1|true false false false")
 run() {
   IFS='|' read -r defs tmpl <<< "$1"
+  defs="$defs ${SPEC_EXTRA:-}"
   out=$(bash "$R/scripts/spec_regs.sh" "$defs" $tmpl 2>&1)
   if echo "$out" | grep -q "error"; then echo "FAIL [$tmpl] $defs: $(echo "$out" | grep error | head -1)"; else echo "ok   [$tmpl] $defs"; fi
 }
-export -f run; export R
+export -f run; export R SPEC_EXTRA
 printf '%s\n' "${cases[@]}" | xargs -P "$J" -I{} bash -c 'run "$@"' _ {} > /tmp/spec_matrix.out
 grep FAIL /tmp/spec_matrix.out; n=$(grep -c FAIL /tmp/spec_matrix.out); echo "$(grep -c '^ok' /tmp/spec_matrix.out) ok, $n failed"; [ "$n" = 0 ]
