@@ -16,6 +16,7 @@ for c in c3 c3cone c4 c4csg c5; do
 done
 cp $SRC/bench_default.json $DST/bench_c3.json
 cp $SRC/rocprof_bench.json $SRC/smoke.log $DST/
+cp $SRC/bench_c3_rocprof_spans.json $DST/ 2>/dev/null || true
 cp $SRC/rocprof/c3_kernel_stats.csv $DST/kernel_stats_c3.csv
 cp $SRC/rocprof/c3_kernel_trace.csv $DST/kernel_trace_c3.csv
 python3 scripts/trace_span.py $DST/kernel_trace_c3.csv 30 $DST/trace_span_c3.json > /dev/null
