@@ -2094,7 +2094,12 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     held_px = ~0u;
   };
   // work sharing (RT_SHARE): per-lane sample bookkeeping in Bd->lw (Board)
-  const int wave = (int)(threadIdx.x >> 6);
+// the wave index through readfirstlane (an SGPR) in the BVH and CSG kernels:
+// C4 -1.0 %, c4csg -2.2 %; C3 +0.5..1.2 %, C2 +1.3..2.2 % (profiles/r05/wave_ab/)
+#ifndef RT_WAVE_SGPR
+#define RT_WAVE_SGPR (BVH || CSG)
+#endif
+  const int wave = RT_WAVE_SGPR ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : (int)(threadIdx.x >> 6);
   int my_idle = 0, spins = 0;  // wave-uniform: idle lanes this wave reports, idle rounds
   bool my_active = true;       // wave-uniform: counted in Bd->nactive
   // wave-uniform: the tail has begun for this wave (it drained the queue, or
@@ -2117,12 +2122,42 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off);
   unsigned long long* kcnt = reinterpret_cast<unsigned long long*>(smem + P.cnt_off + CNT_KIND_OFF);
   for (int k = 0; k < RT_NUM_KINDS; k++) kcnt[k * WG + threadIdx.x] = 0;
-  // shadow tests of kind k (per lane)
-  auto cnt_kind = [&](int k, uint64_t v) { atomicAdd(&kcnt[k * WG + threadIdx.x], (unsigned long long)v); };
-  // a unit event on the lanes where b holds (wave-uniform call)
+  // The counters' LDS addresses in the BVH and CSG kernels are formed at each
+  // use from a scalar base that the empty asm hides from loop-invariant
+  // hoisting: hoisted, they were held in VGPRs across the main loop and
+  // spilled, and each pass paid a scratch reload and a vmcnt(0) wait per
+  // counter. C4 -1.0 %, c4csg -0.9 %; the small linear scenes (C3 within
+  // noise, C2 +2 %) keep the plain form (profiles/r05/remat_ab/).
+#ifndef RT_CNT_REMAT
+#define RT_CNT_REMAT (BVH || CSG)
+#endif
+  auto opaque_s = [](uint32_t b) {  // (b is wave-uniform: readfirstlane makes that explicit)
+    b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+    asm volatile("" : "+s"(b));
+    return b;
+  };
+  // shadow tests of kind k (per lane): kcnt[k * WG + threadIdx.x]
+  auto cnt_kind = [&](int k, uint64_t v) {
+    if constexpr (RT_CNT_REMAT) {
+      uint32_t l;  // the lane number from mbcnt at the use (a hoisted one was spilled too)
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+      const uint32_t a = opaque_s((uint32_t)P.cnt_off + (uint32_t)(CNT_KIND_OFF + (k * WG + wave * 64) * 8)) + l * 8u;
+      atomicAdd(reinterpret_cast<unsigned long long*>(smem + a), (unsigned long long)v);
+    } else {
+      atomicAdd(&kcnt[k * WG + threadIdx.x], (unsigned long long)v);
+    }
+  };
+  // a unit event on the lanes where b holds (wave-uniform call): cnt[k * WAVES_PER_WG + wave]
   auto cnt_unit = [&](int k, bool b) {
     const unsigned int n = (unsigned int)__popcll(wave_ballot(b));
-    if (lane == 0 && n) atomicAdd(&cnt[k * WAVES_PER_WG + wave], (unsigned long long)n);
+    if (lane == 0 && n) {
+      if constexpr (RT_CNT_REMAT)
+        atomicAdd(reinterpret_cast<unsigned long long*>(
+                      smem + opaque_s((uint32_t)P.cnt_off + (uint32_t)((k * WAVES_PER_WG + wave) * 8))),
+                  (unsigned long long)n);
+      else
+        atomicAdd(&cnt[k * WAVES_PER_WG + wave], (unsigned long long)n);
+    }
   };
   WaveStack bst;
   bst.mask = reinterpret_cast<uint64_t*>(smem + P.bvh_stack_off) + (threadIdx.x >> 6) * BVH_STACK;
@@ -3416,9 +3451,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const double a = dot(ld, ld);
           const double hb = dot(lo, ld);
           const double disc = hb * hb - a * c;
-          if (jopen[li] && i != hit_i && !(disc < 0.0)) {
+          if (jopen[li] && !(disc < 0.0)) {  // (i != hit_i: see ssphere)
             const double t0 = (-hb - gsqrt(disc)) / a;
-            if (t0 > 0.0 && t0 * rlen < dist_a[li]) {
+            if (t0 > 0.0 && t0 * rlen < dist_a[li] && i != hit_i) {
               jopen[li] = false;
               jsend[li] = i + 1;
             }
@@ -3455,9 +3490,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
               if (!((lonm >> li) & 1)) continue;
               const double hb = dot(lo, uld[li]);
               const double disc = hb * hb - ua[li] * c;
-              if (jopen[li] && i != hit_i && !(disc < 0.0)) {
+              if (jopen[li] && !(disc < 0.0)) {  // (i != hit_i: see ssphere)
                 const double t0 = (-hb - gsqrt(disc)) / ua[li];
-                if (t0 > 0.0 && t0 * rlen < dist_a[li]) {
+                if (t0 > 0.0 && t0 * rlen < dist_a[li] && i != hit_i) {
                   jopen[li] = false;
                   jsend[li] = i + 1;
                 }
@@ -3666,9 +3701,15 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             const double hb = dot(l.o, l.d);
             const double c = dot(l.o, l.o) - 1.0;
             const double disc = hb * hb - a * c;
-            if (open && i != hit_i && !(disc < 0.0)) {
+            // The hit's own object (i == hit_i, raytracer.go:416) is excluded
+            // after the rare real-root branch, not before it: the lane's hit
+            // index is then read only there (the brute-force kernel keeps it in
+            // scratch, and a compare per sphere cost a scratch reload and a
+            // vmcnt(0) wait per sphere and light). Its sqrt and division have
+            // no side effect; verdicts and counts are unchanged.
+            if (open && !(disc < 0.0)) {
               const double t0 = (-hb - gsqrt(disc)) / a;
-              if (t0 > 0.0 && t0 * rlen < dist) {
+              if (t0 > 0.0 && t0 * rlen < dist && i != hit_i) {
                 open = false;
                 send = i + 1;
               }
