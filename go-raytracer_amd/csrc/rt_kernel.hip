@@ -1481,6 +1481,13 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     d[9] = mm.kd;
     d[10] = mm.ks;
     d[11] = mm.specular_exponent;
+    // per-material terms of refract / fresnel, formed here with the device's
+    // operations (correctly rounded either way): 1 / ior (n1 / n2 outside the
+    // object, raytracer.go:438) and ((1 - ior) / (1 + ior))^2 (r0,
+    // raytracer.go:460-461)
+    d[12] = 1.0 / mm.refractive_index;
+    const double r0 = (1.0 - mm.refractive_index) / (1.0 + mm.refractive_index);
+    d[13] = r0 * r0;
   }
   {  // unrolled steps of the device's branch-free specular powering (pow_small_int)
     int maxn = 1;

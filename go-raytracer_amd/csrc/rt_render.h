@@ -3309,6 +3309,9 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         vmrec[9] = r[7];
         vmrec[10] = r[8];
         vmrec[11] = r[9];
+        vmrec[12] = 1.0 / vmrec[8];  // (the host's per-material terms, see rt_set_scene)
+        const double r0 = (1.0 - vmrec[8]) / (1.0 + vmrec[8]);
+        vmrec[13] = r0 * r0;
         surf_bad = bad;
       }
     }
@@ -4055,15 +4058,14 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         double kr = 0.0;
         d3 lw = L;
         if (tmode) {
-          double n1 = 1.0, n2 = M[8];
+          // n1 / n2: 1 / ior from outside (M[12]), ior / 1 = ior from inside
+          double ratio = M[12];
           d3 nn = nw;
           if (dot(ray.d, nn) > 0.0) {
-            n1 = M[8];
-            n2 = 1.0;
+            ratio = M[8];
             nn = scale(nn, -1.0);
           }
           // refract (raytracer.go:438-450)
-          double ratio = n1 / n2;
           double cosI = -dot(nn, ray.d);
           double sinT2 = ratio * ratio * (1.0 - cosI * cosI);
           if (!(sinT2 > 1.0)) {
@@ -4076,9 +4078,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             }
           }
           // fresnel (raytracer.go:456-467) on the unflipped normal
-          double cosi = dot(ray.d, nw) / (len(ray.d) * len(nw));
-          double r0 = (1.0 - M[8]) / (1.0 + M[8]);
-          r0 = r0 * r0;
+          double cosi = dot(ray.d, nw) / (rlen * len(nw));  // (rlen = len(ray.d), above)
+          const double r0 = M[13];  // ((1 - ior) / (1 + ior))^2
           double cost = __builtin_fabs(cosi);
           kr = r0 + (1 - r0) * go_pow(1 - cost, 5);
           lw = scale(L, 1.0 - T);

@@ -1,0 +1,22 @@
+# Round 5: A/B of two library builds (RT_AMD_LIB: build_variants/librtamd_head.so
+# = the last commit, in-tree = the working tree), interleaved rounds over the
+# bench configs; then the full GPU suite on the working tree.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=${O:-gpurun_out/r5_lib_ab}
+mkdir -p $O
+b() {  # name lib config
+  RT_AMD_LIB=$2 timeout -k 10 300 python3 bench.py --config $3 --steps 20 --warmup 3 --cpu-baseline off --companion off > $O/$1.json 2> $O/$1.err || { tail -5 $O/$1.err; return 1; }
+  python3 -c "import json; d=json.load(open('$O/$1.json')); print('%-18s %.4f ms/step' % ('$1', d['ms_per_step']))"
+}
+H=build_variants/librtamd_head.so
+N=go-raytracer_amd/csrc/librtamd.so
+for r in 1 2 3; do b c3_head$r $H c3 && b c3_new$r $N c3 || exit 1; done
+for r in 1 2; do
+  for c in ${CFGS:-c3cone c2 c4csg}; do b ${c}_head$r $H $c && b ${c}_new$r $N $c || exit 1; done
+done
+if [ -z "$NO_TESTS" ]; then
+  timeout -k 10 1000 python3 -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+  tail -1 $O/pytest_gpu.log
+fi
