@@ -4047,7 +4047,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if (hasR) {
           d3 rd = sub(ray.d, scale(nw, 2.0 * dot(ray.d, nw)));
           if (M[6] != 0.0) rd = add(rd, mk(M[4], M[5], 0.0));
-          rr.o = add(pw, scale(nw, 1e-4));
+          rr.o = sorig;  // (= add(pw, scale(nw, 1e-4)), raytracer.go:526)
           rr.d = norm(rd);
         }
         bool tmode = T > 0;

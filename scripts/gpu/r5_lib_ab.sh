@@ -12,8 +12,8 @@ b() {  # name lib config
 }
 H=build_variants/librtamd_head.so
 N=go-raytracer_amd/csrc/librtamd.so
-for r in 1 2 3; do b c3_head$r $H c3 && b c3_new$r $N c3 || exit 1; done
-for r in 1 2; do
+for r in $(seq 1 ${C3_ROUNDS:-3}); do b c3_head$r $H c3 && b c3_new$r $N c3 || exit 1; done
+for r in $(seq 1 ${ROUNDS:-2}); do
   for c in ${CFGS:-c3cone c2 c4csg}; do b ${c}_head$r $H $c && b ${c}_new$r $N $c || exit 1; done
 done
 if [ -z "$NO_TESTS" ]; then
