@@ -444,14 +444,16 @@ __device__ __forceinline__ void scan_records(cdptr base, int r0, int rn, Body&& 
 
 // body(i, tx, ty, tz) for the uniform-scale spheres i = r0 .. r0 + rn - 1 in
 // index order (urec records, UNI_REC doubles: the translations m3 m7 m11):
-// two records per scalar load (one s_load_dwordx16 of 64 B), two pairs in
-// flight as in scan_records -- four spheres tested per wait instead of one,
-// so the record latency hides behind more FP64 work (brute-force C5 band
-// 1.85 -> 1.55 s). Loads may read up to 2G - 1 records past the run (the host
-// pads urec); only indices < r0 + rn reach the body. stop() (wave-uniform) is
-// asked every CHECK objects (a multiple of 2G).
+// G records per scalar load group (pairs: 64 B; quads: 128 B), two groups in
+// flight as in scan_records -- 2G spheres tested per wait instead of one, so
+// the record latency hides behind more FP64 work (brute-force C5 band 1.85 ->
+// 1.55 s with pairs). Loads may read up to 2G - 1 records past the run (the
+// host pads urec with 8); only indices < r0 + rn reach the body. stop()
+// (wave-uniform) is asked every CHECK objects (a multiple of 2G).
 #ifndef RT_UNI_PAIRS
-#define RT_UNI_PAIRS 1
+// quads: C5 band 1.446-1.455 -> 1.385-1.393 s once no sphere test reloads a
+// spill (before that, pairs and quads measured alike; profiles/r05/unigroup_ab/)
+#define RT_UNI_PAIRS 2
 #endif
 // after_rec for scan_uni's 16-dword groups: the dependency goes through a
 // readfirstlane of the record's first dword. Under SGPR pressure (3 lights)
