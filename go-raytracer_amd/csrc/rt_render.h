@@ -69,9 +69,6 @@
 #ifndef RT_SHADOW_CHECK
 #define RT_SHADOW_CHECK 8  // brute-force shadow runs: wave-level "any ray open?" test every N objects
 #endif
-#ifndef RT_BRANCHFREE
-#define RT_BRANCHFREE 0  // straight-line Intersect routines: measured -35M scalar, +45M vector instructions on C3, no faster
-#endif
 #ifndef RT_CULL_NOBRANCH
 #define RT_CULL_NOBRANCH 1  // cull tests combined without short-circuit branches (see CULL_AND)
 #endif
@@ -694,102 +691,17 @@ __device__ __forceinline__ bool quadric_hit(const Ray& l, double& t, int& face, 
 }
 
 
-#if RT_BRANCHFREE
-// Branch-free forms of the tests above: the same operations in the same
-// order, every candidate computed and the reference's accept/reject
-// decisions applied as masks and selects (a rejected candidate's division or
-// sqrt has no side effect). On a SIMD machine a per-lane early return only
-// saves work when the whole wave takes it, while its exec-mask bookkeeping
-// is paid every time; the kernel's cost is its instruction count.
-__device__ __forceinline__ bool sphere_hit_bf(const Ray& l, double& t) {  // raytracer.go:58-104
-  const double a = dot(l.d, l.d);
-  const double hb = dot(l.o, l.d);
-  const double c = dot(l.o, l.o) - 1.0;
-  const double disc = hb * hb - a * c;
-  const double t0 = (-hb - __builtin_sqrt(disc)) / a;
-  t = t0;
-  return !(disc < 0.0) & (t0 > 0.0);
-}
-__device__ __forceinline__ bool plane_hit_bf(const Ray& l, d3 n, double pd, double& t) {  // raytracer.go:164-180
-  const double denom = dot(n, l.d);
-  const double tt = (-pd - dot(n, l.o)) / denom;
-  t = tt;
-  return !(__builtin_fabs(denom) < 1e-6) & !(tt <= 0.0);
-}
-__device__ __forceinline__ bool cube_hit_bf(const Ray& l, double& t, int& face) {  // raytracer.go:214-240
-  bool found = false;
-  double best = 0.0;
-  int bf = 0;
-#pragma unroll
-  for (int f = 0; f < 6; f++) {
-    const int ax = (f < 2) ? 2 : ((f < 4) ? 0 : 1);
-    const bool pos = (f == 1 || f == 3 || f == 4);
-    const double negD = pos ? 1.0 : 0.0;
-    const double dA = ax == 0 ? l.d.x : (ax == 1 ? l.d.y : l.d.z);
-    const double oA = ax == 0 ? l.o.x : (ax == 1 ? l.o.y : l.o.z);
-    const double denom = pos ? dA : -dA;
-    const double tt = (negD - (pos ? oA : -oA)) / denom;
-    const d3 p = add(l.o, scale(l.d, tt));
-    const bool ok = !(__builtin_fabs(denom) < 1e-6) & !(tt <= 0.0) & !(p.x < 0) & !(p.x > 1) & !(p.y < 0) &
-                    !(p.y > 1) & !(p.z < 0) & !(p.z > 1);
-    const bool upd = ok & (!found | (tt < best));
-    best = upd ? tt : best;
-    bf = upd ? f : bf;
-    found = found | ok;
-  }
-  t = best;
-  face = bf;
-  return found;
-}
-__device__ __forceinline__ bool cylinder_hit_bf(const Ray& l, double& t, int& face) {  // raytracer.go:279-337
-  double bestT = __builtin_inf();
-  int bestFace = -1;
-  const double a = l.d.x * l.d.x + l.d.z * l.d.z;
-  const double hb = l.o.x * l.d.x + l.o.z * l.d.z;
-  const double c0 = (l.o.x * l.o.x + l.o.z * l.o.z) - 1.0;
-  const double disc = hb * hb - a * c0;
-  const bool side = (__builtin_fabs(a) > 1e-12) & (disc >= 0.0);
-  const double sq = __builtin_sqrt(disc);
-  const double t0 = (-hb - sq) / a, t1 = (-hb + sq) / a;
-  const double y0 = l.o.y + l.d.y * t0, y1 = l.o.y + l.d.y * t1;
-  const bool h0 = side & (y0 >= 0.0) & (y0 <= 1.0) & (t0 > 0.0) & (t0 < bestT);
-  bestT = h0 ? t0 : bestT;
-  bestFace = h0 ? 0 : bestFace;
-  const bool h1 = side & (y1 >= 0.0) & (y1 <= 1.0) & (t1 > 0.0) & (t1 < bestT);
-  bestT = h1 ? t1 : bestT;
-  bestFace = h1 ? 0 : bestFace;
-  const bool caps = __builtin_fabs(l.d.y) > 1e-12;
-  const double tTop = (1.0 - l.o.y) / l.d.y;
-  const double pxT = l.o.x + l.d.x * tTop, pzT = l.o.z + l.d.z * tTop;
-  const bool hT = caps & (pxT * pxT + pzT * pzT <= 1.0) & (tTop > 0.0) & (tTop < bestT);
-  bestT = hT ? tTop : bestT;
-  bestFace = hT ? 1 : bestFace;
-  const double tBot = -l.o.y / l.d.y;
-  const double pxB = l.o.x + l.d.x * tBot, pzB = l.o.z + l.d.z * tBot;
-  const bool hB = caps & (pxB * pxB + pzB * pzB <= 1.0) & (tBot > 0.0) & (tBot < bestT);
-  bestT = hB ? tBot : bestT;
-  bestFace = hB ? 2 : bestFace;
-  t = bestT;
-  face = bestFace;
-  return bestFace >= 0;
-}
-#endif
+// (branch-free forms of these tests, RT_BRANCHFREE, measured -35 M scalar and
+// +45 M vector instructions on C3 and no faster: removed)
 
 // One SceneObject.Intersect on a world-space ray; k is wave-uniform.
 __device__ __forceinline__ bool object_hit(int k, const double* g, const Ray& r, double& t, int& face) {
   Ray l = to_obj(g, r);
   face = 0;
   // (kinds the specialised scene lacks fold away; the generic build keeps all)
-#if RT_BRANCHFREE
-  if (spec_kind(RT_SPHERE) && k == RT_SPHERE) return sphere_hit_bf(l, t);
-  if (spec_kind(RT_PLANE) && k == RT_PLANE) return plane_hit_bf(l, mk(g[12], g[13], g[14]), g[15], t);
-  if (spec_kind(RT_CUBE) && k == RT_CUBE) return cube_hit_bf(l, t, face);
-  if (spec_kind(RT_CYLINDER) && k == RT_CYLINDER) return cylinder_hit_bf(l, t, face);
-#else
   if (spec_kind(RT_SPHERE) && k == RT_SPHERE) return sphere_hit(l, t);
   if (spec_kind(RT_PLANE) && k == RT_PLANE) return plane_hit(l, mk(g[12], g[13], g[14]), g[15], t);
   if (spec_kind(RT_CUBE) && k == RT_CUBE) return cube_hit(l, t, face);
-#endif
   if (!spec_kind(RT_CYLINDER) && !spec_kind(RT_CONE)) return false;  // unreachable for the scene's kinds
   return quadric_hit(l, t, face, spec_kind(RT_CONE) && (!spec_kind(RT_CYLINDER) || k == RT_CONE));
 }
@@ -845,14 +757,6 @@ __device__ __forceinline__ bool may_hit(F3 o, F3 d, float tmax, DP g, float slac
   const float R = b[3] + slack;
   return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= R * R;
 }
-// may_hit with the ray-independent part precomputed: (ox, oy, oz) = centre -
-// origin, r2 = (radius + slack)^2 -- the same operations, so the same bits.
-__device__ __forceinline__ bool may_hit_oc(float ox, float oy, float oz, float r2, F3 d, float tmax) {
-  float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
-  tc = fminf(fmaxf(tc, 0.0f), tmax);
-  float qx = __builtin_fmaf(-tc, d.x, ox), qy = __builtin_fmaf(-tc, d.y, oy), qz = __builtin_fmaf(-tc, d.z, oz);
-  return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= r2;
-}
 // The culls with the lane's activity folded into the final compare (an
 // inactive lane compares against an unreachable bound), so the result is one
 // compare's lane mask: the wave's any-lane test reads it directly (a && of
@@ -870,12 +774,6 @@ __device__ __forceinline__ bool may_hit_s(bool act, F3 o, F3 d, float tmax, floa
 __device__ __forceinline__ bool may_hit_a(bool act, F3 o, F3 d, float tmax, const double* g, float slack) {
   const float* b = reinterpret_cast<const float*>(g + 12);
   return may_hit_s(act, o, d, tmax, b[0], b[1], b[2], b[3], slack);
-}
-__device__ __forceinline__ bool may_hit_oc_a(bool act, float ox, float oy, float oz, float r2, F3 d, float tmax) {
-  float tc = __builtin_fmaf(ox, d.x, __builtin_fmaf(oy, d.y, oz * d.z));
-  tc = fminf(fmaxf(tc, 0.0f), tmax);
-  float qx = __builtin_fmaf(-tc, d.x, ox), qy = __builtin_fmaf(-tc, d.y, oy), qz = __builtin_fmaf(-tc, d.z, oz);
-  return __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz)) <= (act ? r2 : -1.0f);
 }
 __device__ __forceinline__ float ray_slack(F3 o) {
   return 1e-5f * (1.0f + __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z));
@@ -3332,34 +3230,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
 // (hoisting the plane culls' origin half out of the light loop measured
 // +4.6 % on C3, profiles/r05/c3_ab: not kept)
 #define SH_PLANE_CULL(i, d, tmax) may_hit_plane(sof, d, tmax, SHP(i))
-#ifndef RT_CULL_HOIST
-#define RT_CULL_HOIST 0  // measured: -1.5 % VALU but the live arrays spill (C3 +2 %, C2 -0.5 %)
-#endif
-#if defined(RT_SPEC_NOBJ) && RT_CULL && RT_CULL_HOIST && RT_SPEC_NOBJ <= 8
-#define RT_SHADOW_HOISTED 1
-    // Every light's shadow ray starts at sorig: the origin-to-centre vectors
-    // and padded radii of the bounding-sphere culls are computed once per hit.
-    float cox[RT_SPEC_NOBJ], coy[RT_SPEC_NOBJ], coz[RT_SPEC_NOBJ], cr2[RT_SPEC_NOBJ];
-    {
-      const F3 hof = f3(sorig);
-      const float hslack = ray_slack(hof);
-#pragma unroll
-      for (int i = 0; i < RT_SPEC_NOBJ; i++) {
-        if (spec_kinds[i] == RT_PLANE) {
-          cox[i] = coy[i] = coz[i] = cr2[i] = 0.0f;
-          continue;
-        }
-        const float* b = reinterpret_cast<const float*>(S.geo + (size_t)i * GEO + 12);
-        cox[i] = b[0] - hof.x;
-        coy[i] = b[1] - hof.y;
-        coz[i] = b[2] - hof.z;
-        const float R = b[3] + hslack;
-        cr2[i] = R * R;
-      }
-    }
-#else
-#define RT_SHADOW_HOISTED 0
-#endif
+// (the culls' origin-to-centre vectors hoisted out of the light loop
+// measured -1.5 % VALU but C3 +2..3 % from spills: not kept)
     uint32_t sc0 = 0, sc1 = 0, sc2 = 0, sc3 = 0;  // this hit's shadow tests per kind (cones: below)
     // Direction and distance to a light (raytracer.go:378-380).
     auto light_dir = [&](auto lt, d3& ldir, double& dist) {
@@ -3371,44 +3243,17 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         ldir = norm_len(lth, dist);  // dist = len(lth)
       }
     };
-#ifndef RT_LIGHT_SPLIT
-#define RT_LIGHT_SPLIT 0  // lighting after all shadow verdicts (measured: +2.4% VALU instructions)
-#endif
+// (lighting after all shadow verdicts, RT_LIGHT_SPLIT, measured +2.4 % VALU
+// instructions: removed)
 #ifdef RT_SPEC_NLIGHTS
     // Specialised: every light's direction up front -- independent sqrt and
     // division chains the scheduler interleaves -- and the light loop unrolled.
     d3 ldir_a[RT_SPEC_NLIGHTS];
     double dist_a[RT_SPEC_NLIGHTS];
-    bool open_a[RT_SPEC_NLIGHTS];
-#ifndef RT_LIGHT_FIX_SHARED
-#define RT_LIGHT_FIX_SHARED 0  // measured: -0.5 % SALU, +0.3 % VALU, C3 +0.2..1 %: not kept
-#endif
-#if RT_LIGHT_FIX_SHARED && RT_FAST_NORM == 2
-    if constexpr (!spec_feat(SF_LDIR)) {
-      // point lights only: all directions branch-free, one shared fix-up branch
-      bool ok_all = true;
-#pragma unroll
-      for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-        const auto lt = LTP(li);
-        bool ok;
-        ldir_a[li] = norm_len_core(sub(mk(lt[0], lt[1], lt[2]), pw), dist_a[li], ok);
-        ok_all = ok_all & ok;
-      }
-      if (__builtin_expect(!ok_all, 0)) {
-#pragma unroll
-        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-          const auto lt = LTP(li);
-          ldir_a[li] = norm_len_fix(sub(mk(lt[0], lt[1], lt[2]), pw), dist_a[li]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(LTP(li), ldir_a[li], dist_a[li]);
-    }
-#else
+    // (one shared fix-up branch for all lights' normalisations measured
+    // C3 +0.2..1 %: not kept)
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) light_dir(LTP(li), ldir_a[li], dist_a[li]);
-#endif
     PH_MARK(5);
 // (at most 4 lights: with 5-8 the joint sweep's per-light state broke the
 // backend -- "illegal VGPR to SGPR copy", which aborts the process inside
@@ -3539,112 +3384,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       }
     }
 #endif
-#ifndef RT_JOINT_CULL
-#define RT_JOINT_CULL 0  // small specialised scenes: one culled sweep for all shadow rays of a hit (register spills: off)
-#endif
-#if defined(RT_SPEC_NOBJ) && RT_CULL && RT_JOINT_CULL
-#define RT_JOINT_SMALL 1
-    // Small specialised scenes: one sweep over the objects for every light's
-    // shadow ray of this hit (inShadow per light, raytracer.go:411-429, each
-    // stopping at its own first occluder in index order). The rays share
-    // their origin sorig, so per object the cull's centre-minus-origin vector
-    // and padded radius (may_hit), a plane cull's f(0) (may_hit_plane), the
-    // object-space origin (rayToObjectSpace's MulPoint, raytracer.go:51-56,
-    // vec.go:298-304) and the Intersect's origin-only term (object_oc) are
-    // formed once, with the operations one to_obj + Intersect per light would
-    // use: verdicts and counts are bit-identical.
-    bool jopen[RT_SPEC_NLIGHTS];
-    int jsend[RT_SPEC_NLIGHTS];
-    {
-      const F3 sof = f3(sorig);
-      const float sslack = ray_slack(sof);
-      F3 jdf[RT_SPEC_NLIGHTS];
-      float jtmax[RT_SPEC_NLIGHTS];
-#pragma unroll
-      for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-        jopen[li] = hit;
-        jsend[li] = P.nobj;
-        jdf[li] = f3(ldir_a[li]);
-#if RT_STMAX_F32
-        jtmax[li] = (float)dist_a[li] * rlen_rcpf * 1.0001f + 1e-4f;
-#else
-        jtmax[li] = (float)(dist_a[li] / rlen) * 1.0001f + 1e-4f;
-#endif
-      }
-#pragma unroll
-      for (int i = 0; i < RT_SPEC_NOBJ; i++) {
-        const int k = spec_kinds[i];
-#if RT_SPEC_SGEO
-        double gl[GEO];
-#pragma unroll
-        for (int q = 0; q < GEO; q++) gl[q] = sgeo[i * GEO + q];
-        const double* g = gl;
-#else
-        const double* g = S.geo + (size_t)i * GEO;
-#endif
-        bool tst[RT_SPEC_NLIGHTS];
-        bool anyt = false;
-        if (k != RT_PLANE) {
-          const float* b = reinterpret_cast<const float*>(g + 12);
-          const float ox = b[0] - sof.x, oy = b[1] - sof.y, oz = b[2] - sof.z;
-          const float R = b[3] + sslack;
-          const float r2 = R * R;
-#pragma unroll
-          for (int li = 0; li < RT_SPEC_NLIGHTS; li++)
-            tst[li] = may_hit_oc_a(CULL_AND(jopen[li], i != hit_i), ox, oy, oz, r2, jdf[li], jtmax[li]);
-        } else {
-          const double* sh = S.shade + (size_t)i * SHD;
-          const PlaneO po = may_hit_plane_o(sof, sh);
-#pragma unroll
-          for (int li = 0; li < RT_SPEC_NLIGHTS; li++)
-            tst[li] = CULL_AND(CULL_AND(jopen[li], i != hit_i), may_hit_plane_d(po, jdf[li], jtmax[li], sh));
-        }
-#pragma unroll
-        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) anyt = anyt || tst[li];
-        if (!wave_any(anyt)) continue;
-#ifdef RT_EXACT_DIAG
-#pragma unroll
-        for (int li = 0; li < RT_SPEC_NLIGHTS; li++) EXDIAG(k, 1, tst[li]);
-#endif
-        if (CSG && k == RT_CSG) {
-#pragma unroll
-          for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-            if (tst[li]) {
-              Ray sr;
-              sr.o = sorig;
-              sr.d = ldir_a[li];
-              double t;
-              int f;
-              if (csg_hit(CSG_ARGS, P.nobj, CSG_G(i, g), sr, t, f, rlen, dist_a[li], false) && t * rlen < dist_a[li]) {
-                jopen[li] = false;
-                jsend[li] = i + 1;
-              }
-            }
-          }
-          continue;
-        }
-        if (anyt) {
-          Ray l;
-          l.o = to_obj_o(g, sorig);
-          const double oc = object_oc(k, g, l.o);
-#pragma unroll
-          for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-            if (tst[li]) {
-              l.d = to_obj_d(g, ldir_a[li]);
-              double t;
-              int f;
-              if (object_hit_l(k, g, l, oc, t, f) && t * rlen < dist_a[li]) {
-                jopen[li] = false;
-                jsend[li] = i + 1;
-              }
-            }
-          }
-        }
-      }
-    }
-#else
-#define RT_JOINT_SMALL 0
-#endif
+// (one culled sweep over the objects for every light's shadow ray of a hit,
+// RT_JOINT_CULL, measured C3 +6 % from 38 spilled VGPRs: removed)
 #pragma unroll
     for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
       const auto lt = LTP(li);
@@ -3652,7 +3393,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       const d3 ldir = ldir_a[li];
       const double dist = dist_a[li];
 #else
-#define RT_JOINT_SMALL 0
     for (int li = 0; li < P.nlights; li++) {
       const auto lt = LTP(li);
       const int lkind = (int)lt[9];  // wave-uniform
@@ -3680,15 +3420,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       int send = P.nobj;
       if constexpr (!BVH) {
 #ifdef RT_SPEC_NOBJ
-#if RT_JOINT_SMALL
-        open = jopen[li];  // the joint sweep above
-        send = jsend[li];
-        constexpr int SH_NOBJ = 0;
-#else
-        constexpr int SH_NOBJ = RT_SPEC_NOBJ;
-#endif
 #pragma unroll
-        for (int i = 0; i < SH_NOBJ; i++) {
+        for (int i = 0; i < RT_SPEC_NOBJ; i++) {
           if (!wave_any(open)) break;
           const int k = spec_kinds[i];
 #else
@@ -3794,11 +3527,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
           const double* g = S.geo + (size_t)i * GEO;
 #endif
           bool test = CULL_AND(open, i != hit_i);
-#if RT_SHADOW_HOISTED
-          test = k != RT_PLANE ? may_hit_oc_a(test, cox[i], coy[i], coz[i], cr2[i], sdf, stmax)
-                               : CULL_AND(test, may_hit_plane(sof, sdf, stmax, SHP(i)));
-          if (!wave_any(test)) continue;
-#elif RT_CULL
+#if RT_CULL
           test = k != RT_PLANE ? may_hit_a(test, sof, sdf, stmax, g, sslack)
                                : CULL_AND(test, SH_PLANE_CULL(i, sdf, stmax));
           if (!wave_any(test)) continue;
@@ -3975,40 +3704,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
         if (spec_kind(5) && (P.kind_mask & 32)) cnt_kind(5, S.pref[(size_t)send * PREF + 5] - (hk == 5 ? 1u : 0u));
       }
       PH_MARK(6);
-#if defined(RT_SPEC_NLIGHTS) && RT_LIGHT_SPLIT
-      open_a[li] = hit && open;
-      (void)lkind;
-    }
-    // Lighting once every shadow verdict is known: the lights' half vectors
-    // and specular powers are independent chains, formed for every lane, and
-    // the terms are added in light order only where the light is visible
-    // (identical arithmetic to the per-light loop below).
-    double ndl_a[RT_SPEC_NLIGHTS], spec_a[RT_SPEC_NLIGHTS], pow_a[RT_SPEC_NLIGHTS];
-    bool pok_a[RT_SPEC_NLIGHTS];
-#pragma unroll
-    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-      ndl_a[li] = go_max0(dot(nw, ldir_a[li]));
-      const d3 H = norm(add(neg(ray.d), ldir_a[li]));
-      spec_a[li] = go_max0(dot(nw, H));
-      pow_a[li] = pow_small_int(spec_a[li], M[11], pok_a[li]);
-    }
-#pragma unroll
-    for (int li = 0; li < RT_SPEC_NLIGHTS; li++) {
-      const auto lt = LTP(li);
-      if (open_a[li]) {
-        d3 lcol = mk(lt[3], lt[4], lt[5]);
-        if (spec_feat(SF_LSPOT) && (int)lt[9] == RT_LIGHT_SPOT) {  // extension: cone falloff
-          const double ca = dot(neg(ldir_a[li]), mk(lt[6], lt[7], lt[8]));
-          lcol = scale(lcol, ca >= lt[10] ? go_pow(ca, lt[11], (int)G[11]) : 0.0);
-        }
-        d3 diffuse = scale(lcol, ndl_a[li] * M[9]);
-        const double pw_s = pok_a[li] ? pow_a[li] : go_pow(spec_a[li], M[11], (int)G[11]);
-        d3 specular = scale(lcol, M[10] * pw_s);
-        L = add(add(L, diffuse), specular);
-      }
-    }
-    PH_MARK(7);
-#else
       if (hit && open) {
         d3 lcol = mk(lt[3], lt[4], lt[5]);
         if (spec_feat(SF_LSPOT) && lkind == RT_LIGHT_SPOT) {  // extension: cone falloff
@@ -4024,7 +3719,6 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
       }
       PH_MARK(7);
     }
-#endif
     if (hit) {
       if (spec_kind(0) && (P.kind_mask & 1)) cnt_kind(0, sc0);
       if (spec_kind(1) && (P.kind_mask & 2)) cnt_kind(1, sc1);
