@@ -1791,9 +1791,12 @@ static int order_for(rt_context* c, int y0, int trow0, int stride, int tiles_x, 
   // frame-stack lines -- and starts every SIMD on deep glass trees at once:
   // C3 4.14 vs 3.89 ms with the quarter, 3.95-4.04 ms unordered; C4 5.66 /
   // 5.35 / 6.07 ms; quarters of 1/8 and 1/2, and the quarter kept in tile
-  // order, measured no better (profiles/r03/order). RT_ORDER_TOP=d
-  // (environment, experiments): the costliest 1/d first, d = 1 sorts all.
-  static const int topd = getenv("RT_ORDER_TOP") ? std::max(1, atoi(getenv("RT_ORDER_TOP"))) : 4;
+  // order, measured no better (profiles/r03/order). Round 5 (two frames in
+  // flight): the costliest sixth instead of the quarter, c4csg 10.01-10.06 ->
+  // 9.96-9.99 ms, C3 3.013-3.016 -> 2.991-3.010 ms (an eighth: c4csg 9.94-9.98,
+  // C3 3.021-3.026; profiles/r05/order_ab/). RT_ORDER_TOP=d (environment,
+  // experiments): the costliest 1/d first, d = 1 sorts all.
+  static const int topd = getenv("RT_ORDER_TOP") ? std::max(1, atoi(getenv("RT_ORDER_TOP"))) : 6;
   // RT_ORDER_TAIL=d (experiments): the cheapest 1/d of the tiles go last, in
   // tile order, so waves that run out of work early finish on short tiles.
   // Measured slower: C3 3.53-3.56 vs 3.43 ms, C4 5.25-5.29 vs 5.16 (d = 4, 8,
