@@ -1,6 +1,10 @@
 # Round 5: A/B of two library builds (RT_AMD_LIB: build_variants/librtamd_head.so
 # = the last commit, in-tree = the working tree), interleaved rounds over the
-# bench configs; then the full GPU suite on the working tree.
+# bench configs; then the full GPU suite on the working tree. Make the
+# baseline library first, in the CPU container:
+#   git stash && make -C go-raytracer_amd/csrc && cp go-raytracer_amd/csrc/librtamd.so \
+#     build_variants/librtamd_head.so && git stash pop && make -C go-raytracer_amd/csrc
+# Knobs: C3_ROUNDS (3), ROUNDS (2), CFGS ("c3cone c2 c4csg"), NO_TESTS.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
