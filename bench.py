@@ -10,7 +10,8 @@ batch of N frames, one per GPU, with no data-path collective. One process per
 GPU. Workload = config C3 (3840x2160, depth 6, cylinder + cube +
 sphere-for-cone, 4 lights).
 
-Frames in flight (--inflight F, default 2): each rank holds F render contexts
+Frames in flight (--inflight F; default 2, 3 for C3 shares at >= 4 ranks,
+inflight_default): each rank holds F render contexts
 with the scene and launches consecutive steps on them round-robin, one stream
 each, so the next frame's workgroups take the CUs the current frame's last
 waves leave idle. Each step still renders its whole frame (or share) into its
@@ -66,10 +67,11 @@ def parse():
     p.add_argument("--companion", choices=["auto", "off"], default="auto",
                    help="c3: also time c3cone (C3 with the cone) for the line's c3cone field; "
                         "off in profiling runs, whose counters must come from C3 frames only")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight per rank: F render contexts with the same scene on F streams "
                         "render consecutive frames round-robin, so one frame's tail overlaps the next "
-                        "frame's head (every frame still rendered whole; 1 = serial launches)")
+                        "frame's head (every frame still rendered whole; 1 = serial launches). Default "
+                        "(inflight_default): 2, or 3 for the C3 scenes' strong-scaling shares at >= 4 ranks")
     p.add_argument("--schedule", choices=["auto", "pixel", "quads", "pairs"], default="auto",
                    help="rt_set_schedule: how pixels are dealt to lanes (identical pixels and counters); "
                         "auto picks from depth, pixels per lane and frames in flight. The PMC passes run "
@@ -86,6 +88,19 @@ def parse():
                    help="CPU test of the N-rank launch and telemetry path: gloo ranks, synthetic "
                         "per-rank times, no device (tests/test_bench_launch.py)")
     return p.parse_args()
+
+
+def inflight_default(args, world):
+    """Frames in flight when --inflight is not given: 2, and 3 for C3 / c3cone
+    shares of a strong-scaling frame over >= 4 ranks. A share there is 5-10
+    pixels per lane, so its last deep-glass pixels leave the device idle for
+    longer relative to the share, and a third frame fills that tail: the
+    1-GPU rehearsal of every rank's C3 share (scripts/inflight_emul.py,
+    profiles/r05/share_f3/) gives 8 ranks 0.446-0.451 -> 0.425-0.427 ms and
+    4 ranks 0.824-0.838 -> 0.810-0.815 ms, while whole frames (3.04 vs 2.99 ms)
+    and C4's shares are slower with three."""
+    small_linear = args.config in ("c3", "c3cone") and args.rows is None and args.accel != "none"
+    return 3 if (args.scaling == "strong" and world >= 4 and small_linear) else 2
 
 
 def spawn_ranks(n):
@@ -380,6 +395,8 @@ def main():
         kw["height"] = args.height
     rargs = cfg(**kw)
     packed = pkg.scene.convert(rargs)
+    if args.inflight is None:
+        args.inflight = inflight_default(args, world)
     if args.inflight < 1:
         raise SystemExit("--inflight must be >= 1")
     ctxs = make_contexts(pkg, dev, packed, args.inflight, args.specialize == "on",

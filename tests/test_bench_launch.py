@@ -34,3 +34,26 @@ def test_bench_rank_failure_stops_the_launch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "nope"],
                        env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode != 0
+
+
+def test_inflight_default():
+    """Frames in flight when --inflight is not given: 2, and 3 for the C3
+    scenes' strong-scaling shares at >= 4 ranks (bench.inflight_default)."""
+    import argparse
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def ns(**kw):
+        d = dict(config="c3", rows=None, accel="bvh", scaling="strong")
+        d.update(kw)
+        return argparse.Namespace(**d)
+
+    assert bench.inflight_default(ns(), 1) == 2
+    assert bench.inflight_default(ns(), 2) == 2
+    assert bench.inflight_default(ns(), 4) == 3
+    assert bench.inflight_default(ns(), 8) == 3
+    assert bench.inflight_default(ns(config="c3cone"), 8) == 3
+    assert bench.inflight_default(ns(config="c4"), 8) == 2
+    assert bench.inflight_default(ns(config="c4csg"), 8) == 2
+    assert bench.inflight_default(ns(scaling="weak"), 8) == 2
+    assert bench.inflight_default(ns(accel="none"), 8) == 2
