@@ -125,12 +125,14 @@ def test_frames_in_flight_equal_serial_frames(inflight):
             c.close()
 
 
-def test_rccl_pipelined_gathers_with_frames_in_flight(nccl_group):
-    """The strong-scaling loop with two contexts in flight: each RCCL gather is
-    issued on its render's stream; every gathered frame equals the full render."""
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_rccl_pipelined_gathers_with_frames_in_flight(nccl_group, inflight):
+    """The strong-scaling loop with two or three contexts in flight (bench.py
+    uses three for C3 shares at >= 4 ranks): each RCCL gather is issued on its
+    render's stream; every gathered frame equals the full render."""
     import torch
     packed = rt.scene.convert(rt.configs.c3(width=320, height=180))
-    ctxs = [rt.RenderContext(0) for _ in range(2)]
+    ctxs = [rt.RenderContext(0) for _ in range(inflight)]
     try:
         for c in ctxs:
             c.set_scene(packed)
@@ -144,7 +146,9 @@ def test_rccl_pipelined_gathers_with_frames_in_flight(nccl_group):
                 got.append(dr.frame.cpu().numpy())
         got.append(dr.flush().cpu().numpy())
         torch.cuda.synchronize()
-        assert len(got) == 4
+        # a buffer's gather completes when the buffer comes round again (steps
+        # F .. 4), plus the flush
+        assert len(got) == 5 - inflight + 1
         for g in got:
             assert np.array_equal(g, full)
     finally:
