@@ -34,6 +34,7 @@
 
 #include <dlfcn.h>
 #include <hip/hiprtc.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -617,6 +618,8 @@ struct Rtc {
   decltype(&hiprtcGetCode) code = nullptr;
   decltype(&hiprtcDestroyProgram) destroy = nullptr;
   decltype(&hiprtcGetErrorString) errstr = nullptr;
+  // the private namespace's copy of libc's environment pointer (see rtc_sync_env)
+  char*** env = nullptr;
 };
 
 struct SpecCode {
@@ -661,8 +664,27 @@ bool rtc_load() {
   RTC_SYM(destroy, "hiprtcDestroyProgram")
   RTC_SYM(errstr, "hiprtcGetErrorString")
 #undef RTC_SYM
+  // The namespace has its own libc, whose environment pointer was set once,
+  // when the namespace was created. The host process's setenv / unsetenv
+  // (Python's os.environ, pytest's PYTEST_CURRENT_TEST) reallocate the
+  // environment array and free the old one, so the private copy can dangle,
+  // and the compiler reading its environment then crashed the process (a
+  // segfault inside rt_set_scene, seen once in a full GPU test run).
+  // rtc_sync_env points it at the host's current array before every call.
+  Lmid_t lm;
+  if (dlinfo(h, RTLD_DI_LMID, &lm) == 0) {
+    if (void* lc = dlmopen(lm, "libc.so.6", RTLD_NOW | RTLD_NOLOAD)) {
+      r.env = reinterpret_cast<char***>(dlsym(lc, "__environ"));
+      if (!r.env) r.env = reinterpret_cast<char***>(dlsym(lc, "environ"));
+    }
+  }
   g_rtc = r;
   return true;
+}
+
+// Caller holds g_spec_mu (see Rtc::env).
+void rtc_sync_env() {
+  if (g_rtc.env) *g_rtc.env = environ;
 }
 
 
@@ -891,6 +913,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
                            (sk.quads == SCH_QUADS ? "true" : "false") + ">";
   const char* name_expr = name.c_str();
   hiprtcProgram prog;
+  rtc_sync_env();
   hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
                                 k_jit_names);
   if (r != HIPRTC_SUCCESS) return fail(RT_E_DEVICE, std::string("hiprtcCreateProgram: ") + g_rtc.errstr(r));
