@@ -5,7 +5,8 @@ sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
-RT_ABI_VERSION = 5  # include/rt_abi.h
+RT_ABI_VERSION = 6  # include/rt_abi.h
+RT_MAX_DEVICES = 16
 RT_EXP_AMD64_FMA, RT_EXP_AMD64, RT_EXP_PORTABLE = 0, 1, 2  # rt_scene.exp_mode
 
 RT_OK = 0
@@ -26,6 +27,8 @@ RT_SCHED_AUTO, RT_SCHED_PIXEL, RT_SCHED_QUADS, RT_SCHED_PAIRS = 0, 1, 2, 3  # rt
 RT_INFO_LDS, RT_INFO_BVH, RT_INFO_CSG, RT_INFO_STREAM, RT_INFO_WAVEFRONT, RT_INFO_ORDERED = 1, 2, 4, 8, 16, 32  # rt_scene_info
 RT_INFO_SHARE_DEVICE = 64
 RT_SHARE_OFF, RT_SHARE_GROUP, RT_SHARE_DEVICE, RT_SHARE_AUTO = 0, 1, 2, 3  # rt_set_work_sharing
+RT_GATHER_AUTO, RT_GATHER_HOST, RT_GATHER_PEER = 0, 1, 2  # rt_render_opts.gather
+RT_RENDER_DEVICE_LIST, RT_RENDER_OUT_DEVICE, RT_RENDER_GENERIC, RT_RENDER_SPEC_SYNC = 1, 2, 4, 8  # rt_render_opts.flags
 
 
 def RT_SPEC_LIGHTS(n):
@@ -120,6 +123,11 @@ class rt_stats(C.Structure):
         ("shaded_hits", C.c_uint64),
         ("surface_errors", C.c_uint64),
         ("kernel_ms", C.c_double),
+        # ABI 6: rt_render_ex's devices, per-device GPU span, exposed gather time
+        ("devices", C.c_int32),
+        ("reserved2", C.c_int32),
+        ("device_kernel_ms", C.c_double * RT_MAX_DEVICES),
+        ("gather_ms", C.c_double),
     ]
 
     def as_dict(self):
@@ -149,12 +157,27 @@ class rt_render_timing(C.Structure):
         ("bands", C.c_int32),
         ("scene_reused", C.c_int32),
         ("specialized", C.c_int32),
+        ("devices", C.c_int32),
+        ("pending_compiles", C.c_int32),
         ("reserved", C.c_int32),
     ]
 
     def as_dict(self):
         return {k: (round(getattr(self, k), 4) if isinstance(getattr(self, k), float) else int(getattr(self, k)))
                 for k, _ in self._fields_ if k != "reserved"}
+
+
+class rt_render_opts(C.Structure):
+    """rt_render_ex options (ABI 6): devices, gather mode, flags, bands."""
+    _fields_ = [
+        ("device_count", C.c_int32),
+        ("device_mask", C.c_uint32),
+        ("devices", C.c_int32 * RT_MAX_DEVICES),
+        ("gather", C.c_int32),
+        ("flags", C.c_int32),
+        ("bands", C.c_int32),
+        ("reserved", C.c_int32 * 5),
+    ]
 
 
 class PackedScene:

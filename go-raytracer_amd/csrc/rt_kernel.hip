@@ -38,7 +38,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <functional>
+#include <thread>
 #include <cmath>
 #include <array>
 #include <cstdio>
@@ -263,6 +266,10 @@ struct DevScene {
   size_t off_nodes = 0, off_bobj = 0, off_planes = 0, off_runs = 0, off_arec = 0, off_urec = 0;
   double bvh_lo[3] = {0, 0, 0}, bvh_hi[3] = {0, 0, 0};  // padded box of the BVH objects (far_shift)
   int nruns = 0;
+  // host copies of what blob and accel hold: another context (the rt_render
+  // seam's second context, another device) takes the converted scene from
+  // here instead of converting it again (scene_clone)
+  std::vector<char> h_blob, h_accel;
 };
 
 // A sphere whose WorldToObject is a scale + translation (rt_render.h
@@ -551,6 +558,14 @@ struct rt_context {
   std::map<int, hipFunction_t> spec_alt;  // ... for other (schedule, work sharing) pairs (spec_for)
   SpecKey spec_key;                     // what spec_fn was compiled for
   double spec_ms = 0;               // hipRTC compile time of spec_fn (0 = cache hit)
+  // The rt_render seam's contexts compile in the background (spec_build
+  // async): until the scene's kernel is ready, launches run the generic one.
+  bool spec_async = false;
+  bool spec_fallback = false;  // a failed compile leaves the generic kernel instead of failing the launch
+  bool spec_pending = false;   // the scene's specialised kernel is still compiling
+  bool spec_failed = false;    // its compile (or one of a launch's schedule variants) failed
+  std::string spec_err;        // ... with this message
+  bool last_spec = false;      // the last render launch ran a specialised kernel
 };
 
 namespace {
@@ -627,12 +642,25 @@ struct SpecCode {
   std::string lowered;
 };
 
+// Two locks: g_rtc_mu serialises every use of the hipRTC namespace (its
+// loading, the environment copy, a compile: seconds); g_spec_mu guards the
+// caches and the background-compile queue below (held for map lookups only,
+// so a render never waits for a compile it did not ask to wait for).
+std::mutex g_rtc_mu;
 std::mutex g_spec_mu;
 Rtc g_rtc;
-std::map<std::string, SpecCode> g_spec_code;
+std::map<std::string, SpecCode> g_spec_code;  // entries are never erased (references stay valid)
 std::map<std::pair<int, std::string>, hipFunction_t> g_spec_fn;
 
-// Caller holds g_spec_mu.
+// Compile state by key (background queue and failures; guarded by g_spec_mu):
+// a key that failed once fails again at once, in either mode.
+struct SpecJob {
+  int state = 0;    // 0 queued or compiling, 1 compiled, -1 failed
+  std::string err;  // (failed: the compiler's message)
+};
+std::map<std::string, SpecJob> g_jobs;
+
+// Caller holds g_rtc_mu.
 bool rtc_load() {
   if (g_rtc.tried) return g_rtc.create != nullptr;
   g_rtc.tried = true;
@@ -670,7 +698,7 @@ bool rtc_load() {
   // environment array and free the old one, so the private copy can dangle,
   // and the compiler reading its environment then crashed the process (a
   // segfault inside rt_set_scene, seen once in a full GPU test run).
-  // rtc_sync_env points it at the host's current array before every call.
+  // rtc_sync_env gives it a library-owned copy before every compile.
   Lmid_t lm;
   if (dlinfo(h, RTLD_DI_LMID, &lm) == 0) {
     if (void* lc = dlmopen(lm, "libc.so.6", RTLD_NOW | RTLD_NOLOAD)) {
@@ -682,9 +710,28 @@ bool rtc_load() {
   return true;
 }
 
-// Caller holds g_spec_mu (see Rtc::env).
+// The namespace's environment: a deep copy of the host's, owned by the
+// library and never freed (a compile runs for seconds while another host
+// thread may setenv, and the compiler may keep pointers getenv gave it). An
+// unchanged environment reuses the last copy. Caller holds g_rtc_mu.
+struct EnvCopy {
+  std::vector<std::string> s;
+  std::vector<char*> p;
+};
+std::vector<EnvCopy*> g_env_copies;
+
 void rtc_sync_env() {
-  if (g_rtc.env) *g_rtc.env = environ;
+  if (!g_rtc.env) return;
+  std::vector<std::string> cur;
+  for (char** e = environ; e && *e; ++e) cur.emplace_back(*e);
+  if (g_env_copies.empty() || g_env_copies.back()->s != cur) {
+    EnvCopy* c = new EnvCopy;
+    c->s.swap(cur);
+    for (auto& x : c->s) c->p.push_back(&x[0]);
+    c->p.push_back(nullptr);
+    g_env_copies.push_back(c);
+  }
+  *g_rtc.env = g_env_copies.back()->p.data();
 }
 
 
@@ -865,12 +912,41 @@ bool spec_key(const DevScene& s, SpecKey* k) {
 }
 
 // Compile the code object for `key` into g_spec_code (no device needed).
-// Caller holds g_spec_mu.
+// Takes g_rtc_mu for the compile and g_spec_mu for the cache; the caller holds
+// neither.
 int spec_compile(const SpecKey& sk, double* ms) {
   *ms = 0;
   const std::string key = sk.str();
-  if (g_spec_code.count(key)) return RT_OK;
-  if (!rtc_load()) return fail(RT_E_DEVICE, "scene specialisation: " + g_rtc.err);
+  // a key that failed to compile fails again at once (no second compile)
+  auto failed = [&](std::string* err) {
+    auto it = g_jobs.find(key);
+    if (it == g_jobs.end() || it->second.state >= 0) return false;
+    *err = it->second.err;
+    return true;
+  };
+  // every failure is recorded under the key (g_jobs) and reported the same way
+  auto bad = [&](const std::string& msg) {
+    {
+      std::lock_guard<std::mutex> l(g_spec_mu);
+      SpecJob& j = g_jobs[key];
+      j.state = -1;
+      j.err = msg;
+    }
+    return fail(RT_E_DEVICE, "scene specialisation: " + msg);
+  };
+  std::string err;
+  {
+    std::lock_guard<std::mutex> l(g_spec_mu);
+    if (g_spec_code.count(key)) return RT_OK;
+    if (failed(&err)) return fail(RT_E_DEVICE, "scene specialisation: " + err);
+  }
+  std::lock_guard<std::mutex> rl(g_rtc_mu);
+  {
+    std::lock_guard<std::mutex> l(g_spec_mu);  // (compiled by another thread meanwhile)
+    if (g_spec_code.count(key)) return RT_OK;
+    if (failed(&err)) return fail(RT_E_DEVICE, "scene specialisation: " + err);
+  }
+  if (!rtc_load()) return bad(g_rtc.err);
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<std::string> defs = {"-DRT_SPEC_KMASK=" + std::to_string(sk.kmask),
                                    "-DRT_SPEC_FEAT=" + std::to_string(sk.feat)};
@@ -916,7 +992,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
   rtc_sync_env();
   hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
                                 k_jit_names);
-  if (r != HIPRTC_SUCCESS) return fail(RT_E_DEVICE, std::string("hiprtcCreateProgram: ") + g_rtc.errstr(r));
+  if (r != HIPRTC_SUCCESS) return bad(std::string("hiprtcCreateProgram: ") + g_rtc.errstr(r));
   SpecCode sc;
   std::string msg;
   r = g_rtc.add_name(prog, name_expr);
@@ -941,39 +1017,126 @@ int spec_compile(const SpecKey& sk, double* ms) {
     }
   }
   (void)g_rtc.destroy(&prog);
-  if (!msg.empty()) return fail(RT_E_DEVICE, "scene specialisation: " + msg);
-  g_spec_code.emplace(key, std::move(sc));
+  if (!msg.empty()) return bad(msg);
+  {
+    std::lock_guard<std::mutex> l(g_spec_mu);
+    g_spec_code.emplace(key, std::move(sc));
+    auto it = g_jobs.find(key);
+    if (it != g_jobs.end()) it->second.state = 1;
+  }
   *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return RT_OK;
 }
 
-// Compile (or fetch) the specialised LDS/linear kernel for `key` on `device`.
-// Caller holds g_spec_mu.
-int spec_build(int device, const SpecKey& sk, hipFunction_t* fn, double* ms) {
-  *ms = 0;
-  const std::string key = sk.str();
-  auto fit = g_spec_fn.find({device, key});
-  if (fit != g_spec_fn.end()) {
-    *fn = fit->second;
-    return RT_OK;
+// ---------------------------------------------------------------------------
+// Background compiles (the rt_render seam: a first Render() of a new scene
+// shape must not wait for hipRTC). A context in async mode (rt_context
+// spec_async) never compiles on the caller's thread: a missing code object is
+// queued here, the launch renders with the ahead-of-time generic kernel
+// (same pixels and counters), and a later launch switches once the code is
+// ready. One worker thread, started on first use; an atexit handler lets the
+// compile in progress finish before the process tears down the hipRTC
+// namespace under it (at most one compile, ~0.5-2 s).
+// ---------------------------------------------------------------------------
+enum { SPEC_PENDING = 1 };  // internal status of spec_build: queued or compiling
+
+std::vector<SpecKey> g_job_q;  // FIFO of keys to compile; guarded by g_spec_mu
+std::condition_variable g_job_cv;
+std::thread* g_worker = nullptr;
+bool g_worker_stop = false;
+
+void spec_worker() {
+  std::unique_lock<std::mutex> lk(g_spec_mu);
+  for (;;) {
+    g_job_cv.wait(lk, [] { return g_worker_stop || !g_job_q.empty(); });
+    if (g_worker_stop) return;  // (queued jobs are dropped at exit)
+    const SpecKey sk = g_job_q.front();
+    g_job_q.erase(g_job_q.begin());
+    lk.unlock();
+    double ms = 0;
+    (void)spec_compile(sk, &ms);  // records the key's state, compiled or failed, in g_jobs
+    lk.lock();
   }
-  int rc = spec_compile(sk, ms);
+}
+
+// Specialised kernels queued or compiling in the background.
+int spec_jobs_pending() {
+  std::lock_guard<std::mutex> l(g_spec_mu);
+  int n = 0;
+  for (const auto& kv : g_jobs) n += kv.second.state == 0;
+  return n;
+}
+
+void spec_worker_exit() {
+  {
+    std::lock_guard<std::mutex> l(g_spec_mu);
+    g_worker_stop = true;
+  }
+  g_job_cv.notify_all();
+  if (g_worker && g_worker->joinable()) g_worker->join();
+}
+
+// Queue `sk` (caller holds g_spec_mu; the key is not compiled and not queued).
+void spec_enqueue(const SpecKey& sk) {
+  g_jobs[sk.str()] = SpecJob();
+  g_job_q.push_back(sk);
+  if (!g_worker) {
+    g_worker = new std::thread(spec_worker);
+    std::atexit(spec_worker_exit);
+  }
+  g_job_cv.notify_one();
+}
+
+// Compile (or fetch) the specialised kernel for `sk` and load it on `device`.
+// async: a code object not compiled yet is queued for the worker and
+// SPEC_PENDING returned (no wait); a failed background compile returns its
+// error. Takes the locks it needs; the caller holds none.
+int spec_build(int device, const SpecKey& sk, hipFunction_t* fn, double* ms, bool async = false) {
+  *ms = 0;
+  *fn = nullptr;
+  const std::string key = sk.str();
+  {
+    std::lock_guard<std::mutex> l(g_spec_mu);
+    auto fit = g_spec_fn.find({device, key});
+    if (fit != g_spec_fn.end()) {
+      *fn = fit->second;
+      return RT_OK;
+    }
+    if (async && !g_spec_code.count(key)) {
+      auto jit = g_jobs.find(key);
+      if (jit == g_jobs.end()) {
+        spec_enqueue(sk);
+        return SPEC_PENDING;
+      }
+      if (jit->second.state == 0) return SPEC_PENDING;
+      // (state -1: spec_compile reports the recorded failure)
+    }
+  }
+  int rc = spec_compile(sk, ms);  // (a cache hit when the worker compiled it)
   if (rc != RT_OK) return rc;
-  const SpecCode& sc = g_spec_code.at(key);
+  const SpecCode* sc;
+  {
+    std::lock_guard<std::mutex> l(g_spec_mu);
+    sc = &g_spec_code.at(key);
+  }
   DeviceGuard guard(device);
   hipModule_t mod;
-  HIP_TRY(hipModuleLoadData(&mod, sc.code.data()));
+  HIP_TRY(hipModuleLoadData(&mod, sc->code.data()));
   hipFunction_t f;
-  HIP_TRY(hipModuleGetFunction(&f, mod, sc.lowered.c_str()));
-  g_spec_fn[{device, key}] = f;
-  *fn = f;
+  HIP_TRY(hipModuleGetFunction(&f, mod, sc->lowered.c_str()));
+  std::lock_guard<std::mutex> l(g_spec_mu);
+  *fn = g_spec_fn.emplace(std::make_pair(device, key), f).first->second;
   return RT_OK;
 }
 
-// Point c->spec_fn at the specialised kernel of the current scene (or clear it).
+// Point c->spec_fn at the specialised kernel of the current scene (or clear
+// it). In async mode a kernel still compiling leaves spec_fn clear and
+// spec_pending set (launch() retries), and a failed compile sets spec_failed.
 int spec_prepare(rt_context* c) {
   c->spec_fn = nullptr;
   c->spec_ms = 0;
+  c->spec_pending = false;
+  c->spec_failed = false;
   if (!c->specialize || !c->has_scene) return RT_OK;
   SpecKey sk;
   if (!spec_key(c->sc, &sk)) return RT_OK;
@@ -983,13 +1146,39 @@ int spec_prepare(rt_context* c) {
   if (sk.share == RT_SHARE_GROUP && sk.quads == SCH_PAIRS) sk.quads = SCH_QUADS;  // the LDS board assumes one owner lane per pixel
   c->spec_key = sk;
   c->spec_alt.clear();
-  std::lock_guard<std::mutex> lock(g_spec_mu);
-  return spec_build(c->device, sk, &c->spec_fn, &c->spec_ms);
+  const int rc = spec_build(c->device, sk, &c->spec_fn, &c->spec_ms, c->spec_async);
+  if (rc == SPEC_PENDING) {
+    c->spec_pending = true;
+    return RT_OK;
+  }
+  if (rc != RT_OK) {
+    c->spec_failed = true;
+    c->spec_err = g_err;
+  }
+  return rc;
+}
+
+// Queue (async contexts) the specialised variant a launch of `pixels` pixels
+// will ask for when it differs from the scene's own (schedule or sharing), so
+// that it compiles alongside the scene's kernel rather than after it.
+void spec_prefetch(rt_context* c, uint64_t pixels) {
+  if (!c->spec_async || !c->has_scene || !(c->spec_pending || c->spec_fn)) return;
+  int sch = pick_schedule(c->sched, c->sc, pixels, c->cus, c->inflight, true);
+  const int share = pick_share(c->share_mode, c->sc, pixels, c->cus, c->inflight);
+  if (share == RT_SHARE_GROUP && sch == SCH_PAIRS) sch = SCH_QUADS;
+  if (sch == c->spec_key.quads && share == c->spec_key.share) return;
+  SpecKey sk = c->spec_key;
+  sk.quads = sch;
+  sk.share = share;
+  hipFunction_t f = nullptr;
+  double ms = 0;
+  (void)spec_build(c->device, sk, &f, &ms, true);  // queued, or loaded if already compiled
 }
 
 // The specialised kernel for schedule `sch` and work-sharing mode `share`
 // (another pair than the scene's is compiled on first use: a launch covering
-// a small share of the frame).
+// a small share of the frame). In async mode a pair still compiling (or
+// failed) gives *fn = nullptr: this launch runs the generic kernel.
 int spec_for(rt_context* c, int sch, int share, hipFunction_t* fn) {
   if (share == RT_SHARE_GROUP && sch == SCH_PAIRS) sch = SCH_QUADS;
   if (!c->spec_fn || (c->spec_key.quads == sch && c->spec_key.share == share)) {
@@ -1004,9 +1193,16 @@ int spec_for(rt_context* c, int sch, int share, hipFunction_t* fn) {
     sk.share = share;
     double ms = 0;
     hipFunction_t f = nullptr;
-    std::lock_guard<std::mutex> lock(g_spec_mu);
-    int rc = spec_build(c->device, sk, &f, &ms);
-    if (rc != RT_OK) return rc;
+    int rc = spec_build(c->device, sk, &f, &ms, c->spec_async);
+    if (rc == SPEC_PENDING) {
+      *fn = nullptr;
+      return RT_OK;
+    }
+    if (rc != RT_OK && !c->spec_fallback) return rc;
+    if (rc != RT_OK) {  // (the generic kernel from now on for this pair)
+      c->spec_failed = true;
+      c->spec_err = g_err;
+    }
     it = c->spec_alt.emplace(k, f).first;
   }
   *fn = it->second;
@@ -1063,7 +1259,6 @@ int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile
   }
   sk.feat = features & (SF_VM | SF_LDIR | SF_LSPOT);
   sk.nlights = nlights;
-  std::lock_guard<std::mutex> lock(g_spec_mu);
   double ms = 0;
   int rc = spec_compile(sk, &ms);
   if (compile_ms) *compile_ms = ms;
@@ -1192,6 +1387,8 @@ void rt_destroy(rt_context* c) {
 static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntrows, void* d_rgba, void* stream,
                   bool est);
 static int estimate_costs(rt_context* c);
+static bool want_order(const rt_context* c);
+static int scene_install(rt_context* c, DevScene& s, const std::vector<uint32_t>* costs);
 
 int rt_set_scene(rt_context* c, const rt_scene* in) {
   if (!c || !in) return fail(RT_E_INVALID, "rt_set_scene: NULL argument");
@@ -1639,6 +1836,7 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       free_scene(s);
       return rc;
     }
+    s.h_blob.swap(blob);
   }
   s.kinds.assign(kind.begin(), kind.begin() + s.nobj);  // top-level objects (test counts)
   {
@@ -1743,9 +1941,20 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
       free_scene(s);
       return rc;
     }
+    s.h_accel.swap(acc);
     s.nplanes = (int)planes.size();
     s.nnodes = (int)(b.nodes.size() / BN);
   }
+  return scene_install(c, s, nullptr);
+}
+
+// Make the converted scene `s` (blob and accel already on c's device) the
+// context's scene: frame stack and VM records sized for it, the specialised
+// kernel prepared, and the tile costs either estimated (costs == nullptr) or
+// taken from a context holding the same scene (the estimate counts rays,
+// which do not depend on the device or the kernel). On failure s is freed.
+static int scene_install(rt_context* c, DevScene& s, const std::vector<uint32_t>* costs) {
+  const int nprog = s.num_programs;
   // Frame stack: (depth - 1) frames per lane, lane-interleaved per wave slot.
   int frames = std::max(1, s.depth - 1);
   const int waves = c->cus * 8 * WAVES_PER_WG;  // upper bound of any persistent grid
@@ -1775,12 +1984,47 @@ int rt_set_scene(rt_context* c, const rt_scene* in) {
     }
   }
   free_scene(c->sc);
-  c->sc = s;
+  c->sc = std::move(s);
   c->has_scene = true;
   clear_orders(c);
-  int rc = spec_prepare(c);
+  // a failed specialisation still leaves a complete scene (generic kernel,
+  // tile order): the caller may render it (the rt_render seam falls back)
+  const int spec_rc = spec_prepare(c);
+  const std::string spec_msg = g_err;
+  int rc = RT_OK;
+  if (!costs) rc = estimate_costs(c);
+  else if (want_order(c)) c->tile_cost = *costs;
   if (rc != RT_OK) return rc;
-  return estimate_costs(c);
+  if (spec_rc != RT_OK) return fail(spec_rc, spec_msg);
+  return RT_OK;
+}
+
+// Give context c the scene `src` holds (same device or another one): the
+// host copies of src's converted scene uploaded to c's device, src's tile
+// costs reused -- no conversion, BVH build or estimate launch again. Used by
+// the rt_render seam for its second context and for every further device.
+static int scene_clone(rt_context* c, const rt_context* src) {
+  if (!src->has_scene) return fail(RT_E_INVALID, "scene_clone: no scene");
+  DeviceGuard guard(c->device);
+  DevScene s = src->sc;  // (host fields and copies; device pointers replaced below)
+  s.blob = nullptr;
+  s.accel = nullptr;
+  if (hipMalloc((void**)&s.blob, std::max<size_t>(1, s.h_blob.size())) != hipSuccess) {
+    s.blob = nullptr;
+    free_scene(s);
+    return fail(RT_E_NOMEM, "scene_clone: scene blob");
+  }
+  if (hipMalloc((void**)&s.accel, std::max<size_t>(1, s.h_accel.size())) != hipSuccess) {
+    s.accel = nullptr;
+    free_scene(s);
+    return fail(RT_E_NOMEM, "scene_clone: acceleration buffer");
+  }
+  if ((!s.h_blob.empty() && hipMemcpy(s.blob, s.h_blob.data(), s.h_blob.size(), hipMemcpyHostToDevice) != hipSuccess) ||
+      (!s.h_accel.empty() && hipMemcpy(s.accel, s.h_accel.data(), s.h_accel.size(), hipMemcpyHostToDevice) != hipSuccess)) {
+    free_scene(s);
+    return fail(RT_E_DEVICE, "scene_clone: upload");
+  }
+  return scene_install(c, s, &src->tile_cost);
 }
 
 // Tile order for a launch of `tiles_x` x `tiles_y` tiles (rows [y0, y1), or
@@ -1856,6 +2100,10 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   const DevScene& s = c->sc;
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
+  // async contexts (the rt_render seam): switch to the specialised kernel as
+  // soon as its background compile has finished (a failed compile leaves the
+  // generic kernel, spec_failed set)
+  if (c->spec_pending && !est) (void)spec_prepare(c);
   const bool lds = scene_in_lds(s);
   // Dynamic LDS: [scene blob (LDS flavour)] [VM records] [BVH stack]
   // [counters] [drained-head mask] [PCG jump rows] [frame cores of the first lds_levels levels]
@@ -1866,21 +2114,25 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // per-wave object-record stream buffers (global linear scenes, RT_STREAM)
   const int jump_off = qmask_off + 16;  // after the drained-head mask: the sample-0 jump rows
   const int board_off = jump_off + 20 * 4 * (int)sizeof(uint64_t);  // work-sharing board (RT_SHARE)
-  // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
-  // loads instead: no stream buffers)
-  // (tuning builds with RT_SPEC_EXTRA_FLAGS keep the buffers: they may select the LDS stream)
-  static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
-  const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(c->spec_fn && !(c->accel & RT_ACCEL_CULL)));
   const uint64_t launch_pixels = (uint64_t)s.width * (uint64_t)(stride > 0 ? ntrows * TILE : y1 - y0);
   const int sch =
       est ? (int)SCH_SERIAL : pick_schedule(c->sched, s, launch_pixels, c->cus, c->inflight, c->spec_fn != nullptr);
-  // (the estimate launch runs the scene's own sharing mode: no extra compile)
-  const int share_m = c->spec_fn ? (est ? c->spec_key.share : pick_share(c->share_mode, s, launch_pixels, c->cus, c->inflight)) : 0;
+  const int share_m = (c->spec_fn && !est) ? pick_share(c->share_mode, s, launch_pixels, c->cus, c->inflight) : 0;
+  // The tile-cost estimate runs the ahead-of-time generic kernel (serial
+  // samples, no sharing): its rays per tile do not depend on the kernel, and
+  // a specialised variant of the estimate's schedule would be one more hipRTC
+  // compile at scene setup (C1 / C4 / c4csg / canned render with quads: 0.4 -
+  // 1.8 s in round 5).
   hipFunction_t spec = nullptr;  // built for this scene's flavour (spec_key), this schedule and sharing
-  {
+  if (!est) {
     int rc = spec_for(c, sch, share_m, &spec);
     if (rc != RT_OK) return rc;
   }
+  // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
+  // loads instead: no stream buffers; tuning builds with RT_SPEC_EXTRA_FLAGS
+  // keep the buffers: they may select the LDS stream)
+  static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
+  const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(spec && !(c->accel & RT_ACCEL_CULL)));
   // the generic kernels have no pairs flavour: quads instead (same pixels)
   const bool quads = sch == SCH_QUADS || (sch == SCH_PAIRS && !spec);
   const void* kfn = k_kernels[kernel_index(lds, s.use_bvh, s.has_csg, quads)];
@@ -2066,6 +2318,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   HIP_TRY(hipEventRecord(c->ev1, st));
   if (est) return RT_OK;
   c->timed = true;
+  c->last_spec = spec != nullptr;
   uint64_t rows = 0;
   if (stride > 0) {
     for (int j = 0; j < ntrows; j++) {
@@ -2277,6 +2530,8 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
 #endif
   float ms = 0.f;
   if (c->timed && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) out->kernel_ms = ms;
+  out->devices = 1;
+  out->device_kernel_ms[0] = out->kernel_ms;
   if (reset) {
     HIP_TRY(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 64, st));
     HIP_TRY(hipMemsetAsync(c->stats_part, 0, part.size() * sizeof(unsigned long long), st));

@@ -83,6 +83,10 @@ def load_library(path=None):
     l.rt_render.restype = i
     l.rt_render_last_timing.argtypes = [vp]
     l.rt_render_last_timing.restype = i
+    l.rt_render_ex.argtypes = [vp, vp, vp, vp]
+    l.rt_render_ex.restype = i
+    l.rt_debug_assemble.argtypes = [i, i, i, i, vp, vp]
+    l.rt_debug_assemble.restype = i
     if l.rt_abi_version() != abi.RT_ABI_VERSION:
         raise RenderError("librtamd ABI version mismatch")
     _lib = l
@@ -306,6 +310,61 @@ def spec_precompile(kinds, features=0, nlights=0):
     ms = C.c_double()
     _check(lib.rt_spec_precompile(len(kinds), arr, int(features), C.byref(ms)), "rt_spec_precompile")
     return ms.value
+
+
+def render_opts(devices=None, gather="auto", out_device=False, generic=False, spec_sync=False, bands=0):
+    """abi.rt_render_opts for rt_render_ex. devices: None (the current
+    device), an int N (devices 0..N-1) or a list of ordinals (repeats allowed:
+    one GPU rendering several shares, each with its own contexts)."""
+    o = abi.rt_render_opts()
+    flags = 0
+    if isinstance(devices, int):
+        o.device_count = devices
+    elif devices is not None:
+        devices = [int(d) for d in devices]
+        if not 1 <= len(devices) <= abi.RT_MAX_DEVICES:
+            raise ValueError("1..%d devices" % abi.RT_MAX_DEVICES)
+        o.device_count = len(devices)
+        for k, d in enumerate(devices):
+            o.devices[k] = d
+        flags |= abi.RT_RENDER_DEVICE_LIST
+    o.gather = {"auto": abi.RT_GATHER_AUTO, "host": abi.RT_GATHER_HOST, "peer": abi.RT_GATHER_PEER}[gather]
+    flags |= (abi.RT_RENDER_OUT_DEVICE if out_device else 0) | (abi.RT_RENDER_GENERIC if generic else 0) | \
+        (abi.RT_RENDER_SPEC_SYNC if spec_sync else 0)
+    o.flags = flags
+    o.bands = int(bands)
+    return o
+
+
+def render_frame(scene_or_args, devices=None, gather="auto", generic=False, spec_sync=False, bands=0, out=None):
+    """One synchronous frame through rt_render_ex (include/rt_abi.h): the
+    Render() seam over one or several GPUs of this process. Returns (image
+    numpy uint8 [H, W, 4], abi.rt_stats, abi.rt_render_timing). `out`: a
+    caller-owned host array to render into (reused across calls)."""
+    lib = load_library()
+    p = _packed(scene_or_args)
+    if out is None:
+        out = np.empty((p.height, p.width, 4), np.uint8)
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size == p.height * p.width * 4
+    o = render_opts(devices, gather, False, generic, spec_sync, bands)
+    st = abi.rt_stats()
+    _check(lib.rt_render_ex(p.ref(), C.byref(o), out.ctypes.data_as(C.c_void_p), C.byref(st)), "rt_render_ex")
+    tm = abi.rt_render_timing()
+    _check(lib.rt_render_last_timing(C.byref(tm)), "rt_render_last_timing")
+    return out, st, tm
+
+
+def debug_assemble(width, height, shares, bands=0):
+    """The host side of rt_render_ex's multi-device assembly on host buffers
+    (include/rt_abi.h rt_debug_assemble; no device): shares[d] = device d's
+    packed tile rows. Returns the assembled frame."""
+    lib = load_library()
+    shares = [np.ascontiguousarray(s, dtype=np.uint8) for s in shares]
+    ptrs = (C.c_void_p * len(shares))(*[s.ctypes.data for s in shares])
+    out = np.zeros((height, width, 4), np.uint8)
+    _check(lib.rt_debug_assemble(int(width), int(height), len(shares), int(bands), ptrs,
+                                 out.ctypes.data_as(C.c_void_p)), "rt_debug_assemble")
+    return out
 
 
 def Render(scene_or_args, return_stats=False):

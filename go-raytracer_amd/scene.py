@@ -392,11 +392,11 @@ def convert(args: RenderArgs) -> abi.PackedScene:
     sc.materials = C.cast(c_mats, C.POINTER(abi.rt_material))
     sc.num_objects = len(objs)
     sc.num_materials = len(mats)
-    c_code = None
+    c_csg_code = None
     if csg_leaves:
-        c_code = (C.c_int32 * len(csg_code))(*csg_code)
+        c_csg_code = (C.c_int32 * len(csg_code))(*csg_code)
         sc.csg_leaves = C.cast(c_leaves, C.POINTER(abi.rt_object))
-        sc.csg_code = C.cast(c_code, C.POINTER(C.c_int32))
+        sc.csg_code = C.cast(c_csg_code, C.POINTER(C.c_int32))
         sc.num_csg_leaves = len(csg_leaves)
         sc.csg_code_words = len(csg_code)
     packed_progs = None
@@ -424,5 +424,38 @@ def convert(args: RenderArgs) -> abi.PackedScene:
         packed_progs = (c_code, c_consts, c_entry, [sf for sf, _ in programs], args.state)
     sc.exp_mode = int(args.exp_mode)
     packed = abi.PackedScene(sc, c_lights, c_objs, c_mats, packed_progs, c_ext)
-    packed._csg = (c_leaves, c_code)
+    packed._csg = (c_leaves, c_csg_code)  # (kept alive with the scene)
     return packed
+
+
+SCENE_FILE_MAGIC = b"RTSCENE1"
+
+
+def write_scene_file(packed: abi.PackedScene, path):
+    """Serialise an rt_scene for a non-Python host of the C ABI
+    (tests/c/abi_render.c `file` mode): magic, the scalars, then every array
+    the rt_scene points at as raw include/rt_abi.h structs / words, in field
+    order. Little-endian, native struct layout."""
+    import struct
+    s = packed.scene
+
+    def raw(ptr, ctype, n):
+        if n <= 0:
+            return b""
+        return C.string_at(C.cast(ptr, C.c_void_p), C.sizeof(ctype) * n)
+
+    with open(path, "wb") as f:
+        f.write(SCENE_FILE_MAGIC)
+        f.write(struct.pack("<4i", s.width, s.height, s.depth, s.num_lights))
+        f.write(struct.pack("<10d", s.fov, *s.ambient, *s.bg_start, *s.bg_end))
+        f.write(struct.pack("<9i", s.num_objects, s.num_materials, s.num_programs, s.program_code_words,
+                            s.program_const_count, s.exp_mode, s.num_ext_lights, s.num_csg_leaves, s.csg_code_words))
+        f.write(raw(s.lights, abi.rt_point_light, s.num_lights))
+        f.write(raw(s.objects, abi.rt_object, s.num_objects))
+        f.write(raw(s.materials, abi.rt_material, s.num_materials))
+        f.write(raw(s.program_code, C.c_uint32, s.program_code_words if s.num_programs else 0))
+        f.write(raw(s.program_consts, C.c_uint64, s.program_const_count if s.num_programs else 0))
+        f.write(raw(s.program_entry, C.c_int32, s.num_programs))
+        f.write(raw(s.ext_lights, abi.rt_light, s.num_ext_lights))
+        f.write(raw(s.csg_leaves, abi.rt_object, s.num_csg_leaves))
+        f.write(raw(s.csg_code, C.c_int32, s.csg_code_words))

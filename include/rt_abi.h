@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
+#define RT_MAX_DEVICES 16 /* devices one rt_render_ex call may use */
 #define RT_EXP_AMD64_FMA 0
 #define RT_EXP_AMD64 1
 #define RT_EXP_PORTABLE 2
@@ -257,7 +258,17 @@ typedef struct rt_stats {
     uint64_t surface_errors; /* hits whose surface evaluation failed; the
                               * reference panics on the first one
                               * (raytracer.go:499-501) */
-    double kernel_ms;    /* device time of the last render (GPU path)  */
+    double kernel_ms;    /* device time of the last render (GPU path; with
+                          * several devices the slowest device's span)    */
+    /* ABI 6: the devices of the last frame (rt_render / rt_render_ex; 1 for
+     * rt_read_stats) and, per device in rt_render_opts order, the GPU span of
+     * its share of the frame; gather_ms = host wall time from the moment every
+     * device's share had rendered to the frame complete in the caller's
+     * buffer (the gather and copy work the renders did not hide). */
+    int32_t devices;
+    int32_t reserved2;
+    double device_kernel_ms[RT_MAX_DEVICES];
+    double gather_ms;
 } rt_stats;
 
 /* Opaque per-device context: owns the converted scene on the device, the
@@ -382,9 +393,10 @@ int rt_set_tile_order(rt_context *ctx, int enable);
  * posts the samples it has not started and the pending refraction children
  * of its binary (reflect + refract, raytracer.go:512-556) frames, idle lanes
  * of any wave of the group trace them, and the owner joins their colours in
- * the reference's order. Off by default: its code costs every round of the
- * kernel more than the tail gains on the BASELINE configs.
- * Applies to the current scene at once. */
+ * the reference's order. RT_SHARE_AUTO (the default, below) never picks this
+ * workgroup board: its code costs every round of the kernel more than the
+ * tail gains on the BASELINE configs. Applies to the current
+ * scene at once. */
 #define RT_SHARE_OFF 0
 #define RT_SHARE_GROUP 1
 /* RT_SHARE_DEVICE (ABI 5): the board is device-wide, in uncached HBM -- an
@@ -448,20 +460,86 @@ int rt_debug_run_surface(rt_context *ctx, int program, int n, const long long *f
 int rt_ssim_rgba8(rt_context *ctx, const uint8_t *d_a, const uint8_t *d_b, int width, int height,
                   double *out_ssim, void *stream);
 
-/* Convenience, synchronous whole-frame Render() into host memory
- * (width*height*4 bytes, caller-owned, e.g. Go's image.RGBA.Pix): the
- * replacement of func Render(*Scene) image.Image (raytracer.go:589-682).
- * Keeps, per device, two contexts with the last scene (an unchanged scene --
- * byte-equal arrays -- is not converted or uploaded again), a device frame
- * and a pinned bounce buffer; renders the frame as row bands alternating over
- * the two contexts and copies each finished band to rgba_out while later
- * bands render. Scene specialisation (rt_set_specialize) is on: the first
- * call with a new scene shape pays the hipRTC compile, later ones reuse it;
- * if the compile fails the generic kernel renders the same pixels (logged
- * once to stderr); RT_RENDER_SPECIALIZE=0 in the environment keeps the
- * generic kernel. stats may be NULL; stats->kernel_ms is the GPU span of the
- * frame. Includes the scene upload and the PCIe transfer of the image. */
+/* Synchronous whole-frame Render() into host memory (width*height*4 bytes,
+ * caller-owned, e.g. Go's image.RGBA.Pix): the replacement of
+ * func Render(*Scene) image.Image (raytracer.go:589-682), called from the
+ * EvalState.Render hook (evaluator.go:48). Same as rt_render_ex(scene, NULL,
+ * rgba_out, stats): the caller's current HIP device. */
 int rt_render(const rt_scene *scene, uint8_t *rgba_out, rt_stats *stats);
+
+/* ABI 6: Render() over one or several GPUs of this process.
+ *
+ * Devices (first match): device_mask != 0 -> the devices whose bit is set, in
+ * ascending order; else device_count > 0 with RT_RENDER_DEVICE_LIST in flags
+ * -> devices[0 .. device_count) (an ordinal may repeat: the same GPU then
+ * renders several shares at once, each with its own contexts, which exercises
+ * the multi-device path on one GPU); else device_count > 0 -> devices
+ * 0 .. device_count-1; else the caller's current device. opts may be NULL.
+ *
+ * Partition: the frame's 8-row tile rows are dealt
+ * round-robin, tile row t to device t mod N, so every device gets the same
+ * mix of sky, floor and glass; pixels and counters are those of a one-device
+ * frame (RNG state depends only on (x, 20-row strip), raytracer.go:627-634).
+ * Each device renders its share into its own HBM, densely packed, as row
+ * bands alternating over two contexts and streams.
+ *
+ * Gather (the `gather` field):
+ *   RT_GATHER_HOST  each device DMAs each finished band of its share straight
+ *                   to the band's final rows of a pinned frame, over its own
+ *                   PCIe link, and the host copies finished bands on to
+ *                   rgba_out while later bands render (N links in parallel);
+ *   RT_GATHER_PEER  every share is copied to the first device over xGMI
+ *                   (hipMemcpyPeerAsync, peer access enabled where the
+ *                   devices allow it) and de-interleaved there into one
+ *                   frame, which one DMA brings to the host -- or, with
+ *                   RT_RENDER_OUT_DEVICE, which IS rgba_out;
+ *   RT_GATHER_AUTO  (0) HOST for host output, PEER with RT_RENDER_OUT_DEVICE.
+ * flags: RT_RENDER_OUT_DEVICE -- rgba_out is device memory of the first
+ * device (H x 4W bytes); RT_RENDER_GENERIC -- the ahead-of-time kernel only
+ * (no hipRTC); RT_RENDER_SPEC_SYNC -- a new scene shape waits for its
+ * specialised kernel instead of rendering with the generic one meanwhile.
+ * bands: row bands per device (0: one per ~2 M pixels of the share, <= 4;
+ * RT_RENDER_BANDS in the environment overrides the automatic count).
+ *
+ * Kept per device between calls: two contexts with the last scene (an
+ * unchanged scene -- byte-equal arrays -- is not converted, uploaded or
+ * estimated again; a changed one is converted once and cloned to every
+ * context), the share buffer, streams and events; one pinned frame. Scene
+ * specialisation: a call never waits for hipRTC unless RT_RENDER_SPEC_SYNC --
+ * a new shape renders with the generic kernel (same pixels and counters)
+ * while its specialised kernel compiles on a background thread, and later
+ * calls switch to it (rt_render_timing.specialized / .pending_compiles);
+ * a failed compile is logged once and the generic kernel stays;
+ * RT_RENDER_SPECIALIZE=0 in the environment keeps the generic kernel.
+ * stats may be NULL: the counters summed over every device and context;
+ * kernel_ms = the slowest device's GPU span; devices, device_kernel_ms[],
+ * gather_ms as documented at rt_stats. Synchronous; calls are serialised. */
+#define RT_GATHER_AUTO 0
+#define RT_GATHER_HOST 1
+#define RT_GATHER_PEER 2
+#define RT_RENDER_DEVICE_LIST 1
+#define RT_RENDER_OUT_DEVICE 2
+#define RT_RENDER_GENERIC 4
+#define RT_RENDER_SPEC_SYNC 8
+typedef struct rt_render_opts {
+    int32_t device_count;
+    uint32_t device_mask;
+    int32_t devices[RT_MAX_DEVICES];
+    int32_t gather;     /* RT_GATHER_* */
+    int32_t flags;      /* RT_RENDER_* */
+    int32_t bands;      /* row bands per device, 0 = automatic */
+    int32_t reserved[5];
+} rt_render_opts;
+int rt_render_ex(const rt_scene *scene, const rt_render_opts *opts, uint8_t *rgba_out, rt_stats *stats);
+
+/* Diagnostic (tests, no device): the host side of the multi-device assembly
+ * rt_render_ex runs, on host buffers. shares[d] holds device d's share as
+ * rt_render_ex renders it (its tile rows d, d+N, ... of an N-device frame,
+ * packed, stride 4*width, the last tile row clipped to the image); the frame
+ * is assembled into out with exactly the copy plan -- bands, strided DMA
+ * segments, row clipping -- the device path uses, for `bands` bands per
+ * device (0 = automatic). */
+int rt_debug_assemble(int width, int height, int ndev, int bands, const uint8_t *const *shares, uint8_t *out);
 
 /* ABI 5: the parts of the calling thread's last rt_render call, on one host
  * timeline (setup + render_wait + copy_tail = total):
@@ -471,8 +549,11 @@ int rt_render(const rt_scene *scene, uint8_t *rgba_out, rt_stats *stats);
  *                   bands' host copies run inside it)
  *   copy_tail_ms    the last band's DMA and host copy, and the counters
  *   gpu_ms          GPU span of the frame (first band's start to last end)
- * bands: row bands the frame was rendered in; scene_reused: the scene was
- * unchanged; specialized: the specialised kernel rendered it. */
+ * bands: row bands the frame was rendered in (over all devices);
+ * scene_reused: the scene was unchanged; specialized: every launch of the
+ * call ran a specialised kernel. ABI 6: devices of the call; pending_compiles:
+ * specialised kernels still compiling in the background when the call ended
+ * (the call itself rendered with the generic kernel where they were missing). */
 typedef struct rt_render_timing {
     double total_ms;
     double setup_ms;
@@ -482,6 +563,8 @@ typedef struct rt_render_timing {
     int32_t bands;
     int32_t scene_reused;
     int32_t specialized;
+    int32_t devices;
+    int32_t pending_compiles;
     int32_t reserved;
 } rt_render_timing;
 int rt_render_last_timing(rt_render_timing *out);

@@ -9,6 +9,11 @@
  *
  *   abi_render canned  out.rgba   internal/gml/testdata/canned.gml (golden example_canned.png)
  *   abi_render sphere  out.rgba   internal/gml/testdata/sphere.gml (golden example_sphere.png)
+ *   abi_render file scene.bin out.rgba host|peer [device ...]
+ *       any flattened scene, read from the file go_raytracer_amd.scene.write_scene_file
+ *       wrote (the rt_scene scalars and arrays as raw rt_abi.h structs), rendered by
+ *       rt_render_ex (ABI 6) on the listed devices (repeats allowed; none = the
+ *       current device) with the given gather
  *
  * Writes the width*height*4 image.RGBA.Pix bytes and prints the work counters
  * as one JSON line. Build: tests/hip/Makefile (links go-raytracer_amd/csrc/librtamd.so).
@@ -170,9 +175,114 @@ static int sphere(const char *out) {
     return emit(&sc, out);
 }
 
+/* ---- file mode: a serialised rt_scene (go_raytracer_amd/scene.py write_scene_file) ---- */
+static int rd(FILE *f, void *p, size_t n) { return n == 0 || fread(p, 1, n, f) == n; }
+
+static void *rd_array(FILE *f, size_t elem, int32_t n, int *ok) {
+    if (n <= 0) return NULL;
+    void *p = malloc(elem * (size_t)n);
+    if (!p || !rd(f, p, elem * (size_t)n)) *ok = 0;
+    return p;
+}
+
+static int from_file(const char *scene_path, const char *out, const char *gather, int ndev, char **devs) {
+    FILE *f = fopen(scene_path, "rb");
+    if (!f) {
+        fprintf(stderr, "cannot open %s\n", scene_path);
+        return 2;
+    }
+    char magic[8];
+    int32_t hdr[4], cnt[9];
+    double dv[10];
+    int ok = rd(f, magic, 8) && memcmp(magic, "RTSCENE1", 8) == 0 && rd(f, hdr, sizeof hdr) && rd(f, dv, sizeof dv) &&
+             rd(f, cnt, sizeof cnt);
+    rt_scene sc;
+    memset(&sc, 0, sizeof sc);
+    if (ok) {
+        sc.width = hdr[0];
+        sc.height = hdr[1];
+        sc.depth = hdr[2];
+        sc.num_lights = hdr[3];
+        sc.fov = dv[0];
+        for (int k = 0; k < 3; k++) {
+            sc.ambient[k] = dv[1 + k];
+            sc.bg_start[k] = dv[4 + k];
+            sc.bg_end[k] = dv[7 + k];
+        }
+        sc.num_objects = cnt[0];
+        sc.num_materials = cnt[1];
+        sc.num_programs = cnt[2];
+        sc.program_code_words = cnt[3];
+        sc.program_const_count = cnt[4];
+        sc.exp_mode = cnt[5];
+        sc.num_ext_lights = cnt[6];
+        sc.num_csg_leaves = cnt[7];
+        sc.csg_code_words = cnt[8];
+        sc.lights = rd_array(f, sizeof(rt_point_light), sc.num_lights, &ok);
+        sc.objects = rd_array(f, sizeof(rt_object), sc.num_objects, &ok);
+        sc.materials = rd_array(f, sizeof(rt_material), sc.num_materials, &ok);
+        sc.program_code = rd_array(f, sizeof(uint32_t), sc.num_programs ? sc.program_code_words : 0, &ok);
+        sc.program_consts = rd_array(f, sizeof(uint64_t), sc.num_programs ? sc.program_const_count : 0, &ok);
+        sc.program_entry = rd_array(f, sizeof(int32_t), sc.num_programs, &ok);
+        sc.ext_lights = rd_array(f, sizeof(rt_light), sc.num_ext_lights, &ok);
+        sc.csg_leaves = rd_array(f, sizeof(rt_object), sc.num_csg_leaves, &ok);
+        sc.csg_code = rd_array(f, sizeof(int32_t), sc.csg_code_words, &ok);
+    }
+    fclose(f);
+    if (!ok) {
+        fprintf(stderr, "malformed scene file %s\n", scene_path);
+        return 2;
+    }
+    rt_render_opts o;
+    memset(&o, 0, sizeof o);
+    o.gather = !strcmp(gather, "peer") ? RT_GATHER_PEER : RT_GATHER_HOST;
+    if (ndev > RT_MAX_DEVICES) return 2;
+    if (ndev > 0) {
+        o.device_count = ndev;
+        o.flags = RT_RENDER_DEVICE_LIST;
+        for (int i = 0; i < ndev; i++) o.devices[i] = atoi(devs[i]);
+    }
+    size_t bytes = (size_t)sc.width * sc.height * 4;
+    uint8_t *pix = (uint8_t *)malloc(bytes);
+    rt_stats st;
+    if (!pix) return 2;
+    int rc = rt_render_ex(&sc, &o, pix, &st);
+    if (rc != RT_OK) {
+        fprintf(stderr, "rt_render_ex failed (%d): %s\n", rc, rt_last_error());
+        free(pix);
+        return 1;
+    }
+    FILE *g = fopen(out, "wb");
+    if (!g || fwrite(pix, 1, bytes, g) != bytes) {
+        fprintf(stderr, "cannot write %s\n", out);
+        free(pix);
+        return 2;
+    }
+    fclose(g);
+    free(pix);
+    printf("{\"width\": %d, \"height\": %d, \"primary_rays\": %llu, \"secondary_rays\": %llu, \"shadow_rays\": %llu, "
+           "\"shaded_hits\": %llu, \"surface_errors\": %llu, \"tests\": [",
+           sc.width, sc.height, (unsigned long long)st.primary_rays, (unsigned long long)st.secondary_rays,
+           (unsigned long long)st.shadow_rays, (unsigned long long)st.shaded_hits, (unsigned long long)st.surface_errors);
+    for (int k = 0; k < RT_NUM_KINDS; k++) printf("%s%llu", k ? ", " : "", (unsigned long long)st.tests[k]);
+    printf("], \"shadow_tests\": [");
+    for (int k = 0; k < RT_NUM_KINDS; k++) printf("%s%llu", k ? ", " : "", (unsigned long long)st.shadow_tests[k]);
+    printf("], \"devices\": %d, \"device_kernel_ms\": [", st.devices);
+    for (int k = 0; k < st.devices; k++) printf("%s%.4f", k ? ", " : "", st.device_kernel_ms[k]);
+    printf("], \"kernel_ms\": %.4f, \"gather_ms\": %.4f}\n", st.kernel_ms, st.gather_ms);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc >= 5 && !strcmp(argv[1], "file")) {
+        if (rt_abi_version() != RT_ABI_VERSION) {
+            fprintf(stderr, "ABI version mismatch\n");
+            return 2;
+        }
+        return from_file(argv[2], argv[3], argv[4], argc - 5, argv + 5);
+    }
     if (argc != 3) {
-        fprintf(stderr, "usage: %s canned|sphere out.rgba\n", argv[0]);
+        fprintf(stderr, "usage: %s canned|sphere out.rgba | file scene.bin out.rgba host|peer [device ...]\n", argv[0]);
         return 2;
     }
     if (rt_abi_version() != RT_ABI_VERSION) {
