@@ -84,6 +84,16 @@ def parse():
     p.add_argument("--specialize", choices=["on", "off"], default="on",
                    help="scene-specialised kernel for small linear scenes (hipRTC, compiled once "
                         "before the warmup; bit-identical output)")
+    p.add_argument("--api", action="store_true",
+                   help="time the reference's seam instead: ONE process renders each step through rt_render_ex "
+                        "(include/rt_abi.h ABI 6, the Render() replacement) over --gpus N devices (tile rows dealt "
+                        "round-robin, the frame gathered into pageable host memory); no torch.distributed")
+    p.add_argument("--api-devices", default=None, metavar="D0,D1,...",
+                   help="--api: explicit device ordinals (repeats allowed: one GPU rendering several shares, "
+                        "a one-GPU rehearsal of the N-device path)")
+    p.add_argument("--gather", choices=["auto", "host", "peer"], default="auto",
+                   help="--api: host = each device DMAs its share to the pinned frame over its own PCIe link; "
+                        "peer = shares copied to the first device over xGMI, one DMA to the host")
     p.add_argument("--launch-selftest", action="store_true",
                    help="CPU test of the N-rank launch and telemetry path: gloo ranks, synthetic "
                         "per-rank times, no device (tests/test_bench_launch.py)")
@@ -365,8 +375,90 @@ def render_api_leg(pkg, packed, reps=30, budget_s=20.0):
             "rays_per_call": int(st.primary_rays + st.secondary_rays + st.shadow_rays)}
 
 
+def api_main(args):
+    """--api: one step = one synchronous rt_render_ex call (the Render() seam,
+    raytracer.go:589-682, over N GPUs of this process, ABI 6): scene compare,
+    N shares rendered, the gather into a pageable host buffer, the counters.
+    The first call of the process (new scene: conversion, upload, estimate,
+    the generic kernel while the specialised one compiles in the background)
+    is reported apart; then calls until the specialised kernel renders, W
+    warm-up calls and K timed calls. value = rays per call / wall per call."""
+    import numpy as np
+    pkg = load_package()
+    import torch  # noqa: F401  (the HIP runtime the library binds to)
+    devices = [int(x) for x in args.api_devices.split(",")] if args.api_devices else list(range(args.gpus))
+    cfg = pkg.configs.CONFIGS[args.config]
+    kw = {}
+    if args.width:
+        kw["width"] = args.width
+    if args.height:
+        kw["height"] = args.height
+    rargs = cfg(**kw)
+    packed = pkg.scene.convert(rargs)
+    out = np.empty((packed.height, packed.width, 4), np.uint8)
+
+    def call():
+        return pkg.render_frame(packed, devices=devices, gather=args.gather, out=out, generic=args.specialize == "off")
+
+    t0 = time.perf_counter()
+    _, st, tm = call()
+    first = {"ms": round((time.perf_counter() - t0) * 1e3, 3), "parts": tm.as_dict()}
+    calls_to_switch = 1
+    t_lim = time.perf_counter() + 120
+    while not tm.specialized and args.specialize == "on" and time.perf_counter() < t_lim:
+        _, st, tm = call()
+        calls_to_switch += 1
+    for _ in range(args.warmup):
+        call()
+    rays = 0
+    dev_ms = [0.0] * len(devices)
+    span = gather = 0.0
+    spec_all = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, st, tm = call()
+        rays += st.total_rays()
+        span += st.kernel_ms
+        gather += st.gather_ms
+        spec_all = spec_all and bool(tm.specialized)
+        for d in range(len(devices)):
+            dev_ms[d] += st.device_kernel_ms[d]
+    elapsed = time.perf_counter() - t0
+    K = args.steps
+    kavg = span / K
+    flops = pkg.abi.algorithmic_flops(st, len(rargs.lights))
+    achieved = flops / (kavg * 1e-3) / 1e12 if kavg > 0 else 0.0
+    line = {
+        "metric": METRIC, "value": round(rays / elapsed / 1e6, 2), "unit": "Mrays/s",
+        "n_gpus": len(set(devices)), "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "%s: %s" % (args.config, pkg.configs.WORKLOADS[args.config]),
+                   "width": packed.width, "height": packed.height, "depth": rargs.depth,
+                   "rays_per_step": int(rays / K), "devices": devices,
+                   "parallelism": "rt_render_ex: rows%d-interleaved, %s gather, one process" % (len(devices), args.gather),
+                   "kernel": "specialised" if spec_all else "generic (specialisation pending or off)"},
+        "seam": {"what": "rt_render_ex(scene, opts, host RGBA8, stats) per step: scene compare + the N shares + "
+                         "gather into pageable host memory + counters (the Render() seam, raytracer.go:589)",
+                 "first_call_ms": first["ms"], "first_call_parts": first["parts"],
+                 "calls_until_specialised": calls_to_switch,
+                 "device_kernel_ms": [round(v / K, 4) for v in dev_ms],
+                 "gather_ms": round(gather / K, 4), "last_call_parts": tm.as_dict()},
+        "roofline": {"bound": "valu-fp64", "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                     "frac": None, "reference_work_frac": round(achieved / PEAK_FP64_TFLOPS / max(1, len(set(devices))), 4),
+                     "kernel_ms": round(kavg, 4),
+                     "kernel_ms_def": "slowest device's GPU span per call (rt_stats.kernel_ms)",
+                     "traffic": None},
+        "cpu_baseline": None,
+    }
+    if args.cpu_baseline == "auto":
+        line["cpu_baseline"] = cpu_baseline(packed, args.cpu_threads)
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.api:
+        return api_main(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher (torchrun) set the ranks up: start them here, before any
         # GPU call in this process
@@ -417,7 +509,7 @@ def main():
         mode = "band"
     # strong scaling over several ranks: frame k's gather overlaps frame k+1's render
     dr = pkg.dist.DistributedRenderer(ctxs, packed, rank, world, dev, mode=mode, band=band,
-                                      pipeline=args.scaling == "strong")
+                                      pipeline=args.scaling == "strong", gather_timing=True)
 
     def barrier():
         if world > 1:

@@ -33,10 +33,15 @@
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
 #include <hip/hiprtc.h>
+#include <sys/syscall.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -50,6 +55,7 @@
 #include <limits>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -911,9 +917,126 @@ bool spec_key(const DevScene& s, SpecKey* k) {
   return true;
 }
 
-// Compile the code object for `key` into g_spec_code (no device needed).
-// Takes g_rtc_mu for the compile and g_spec_mu for the cache; the caller holds
-// neither.
+// The compile helper next to this library (csrc/rt_spec_cc, built with it):
+// every hipRTC compile runs in a child process, so a compiler abort cannot
+// take the renderer's process down and the host's environment changes cannot
+// reach the compiler. "" when it is missing, unusable (a failed start, then
+// for the rest of the process) or RT_SPEC_INPROC=1 asks for the in-process
+// compiler (hipRTC in a private dlmopen namespace, below).
+std::atomic<int> g_helper_off{0};
+
+std::string spec_helper() {
+  static std::string path;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    Dl_info info;
+    if (dladdr((void*)&rt_abi_version, &info) && info.dli_fname) {
+      std::string lib = info.dli_fname;
+      const size_t k = lib.rfind('/');
+      const std::string p = (k == std::string::npos ? std::string(".") : lib.substr(0, k)) + "/rt_spec_cc";
+      if (access(p.c_str(), X_OK) == 0) path = p;
+    }
+  });
+  const char* e = getenv("RT_SPEC_INPROC");
+  if ((e && atoi(e) != 0) || g_helper_off.load()) return std::string();
+  return path;
+}
+
+// Run the helper for one variant: "" on success (sc filled), else the
+// compiler's message. *unavailable: the helper could not be started at all
+// (the caller then compiles in process). fork + exec like Python's
+// subprocess: the child makes only async-signal-safe calls before execve.
+std::string spec_compile_child(const std::string& helper, const std::vector<const char*>& opts, const std::string& name,
+                               SpecCode* sc, bool* unavailable) {
+  *unavailable = false;
+  const char* td = getenv("TMPDIR");
+  std::string tmpl = std::string(td && *td ? td : "/tmp") + "/rt_spec_XXXXXX";
+  std::vector<char> dbuf(tmpl.begin(), tmpl.end());
+  dbuf.push_back(0);
+  if (!mkdtemp(dbuf.data())) {
+    *unavailable = true;
+    return "mkdtemp failed";
+  }
+  const std::string dir = dbuf.data(), out = dir + "/code", outname = out + ".name", log = dir + "/log";
+  std::vector<const char*> argv = {helper.c_str(), out.c_str(), name.c_str()};
+  argv.insert(argv.end(), opts.begin(), opts.end());
+  argv.push_back(nullptr);
+  std::vector<std::string> envs;  // a snapshot of the environment for the child
+  for (char** e = environ; e && *e; ++e) envs.emplace_back(*e);
+  std::vector<char*> envp;
+  for (auto& x : envs) envp.push_back(&x[0]);
+  envp.push_back(nullptr);
+  auto cleanup = [&] {
+    unlink(out.c_str());
+    unlink(outname.c_str());
+    unlink(log.c_str());
+    rmdir(dir.c_str());
+  };
+  const int lfd = open(log.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0600);
+  const int nfd = open("/dev/null", O_RDONLY | O_CLOEXEC);
+  const pid_t pid = fork();
+  if (pid == 0) {
+    if (nfd >= 0) dup2(nfd, 0);
+    if (lfd >= 0) {
+      dup2(lfd, 1);
+      dup2(lfd, 2);
+    }
+#ifdef SYS_close_range
+    if (syscall(SYS_close_range, 3u, ~0u, 0u) != 0)
+#endif
+      for (int fd = 3; fd < 4096; fd++) close(fd);
+    execve(helper.c_str(), (char* const*)argv.data(), envp.data());
+    _exit(127);
+  }
+  if (lfd >= 0) close(lfd);
+  if (nfd >= 0) close(nfd);
+  if (pid < 0) {
+    cleanup();
+    *unavailable = true;
+    return "fork failed";
+  }
+  int status = 0;
+  pid_t w;
+  do {
+    w = waitpid(pid, &status, 0);
+  } while (w < 0 && errno == EINTR);
+  auto slurp = [](const std::string& path, size_t cap) {
+    std::string t;
+    if (FILE* f = fopen(path.c_str(), "rb")) {
+      char b[65536];
+      size_t n;
+      while (t.size() < cap && (n = fread(b, 1, sizeof b, f)) > 0) t.append(b, n);
+      fclose(f);
+    }
+    return t;
+  };
+  const std::string logtxt = slurp(log, 1 << 16);
+  std::string code = slurp(out, (size_t)1 << 30), lowered = slurp(outname, 4096);
+  cleanup();
+  const bool exited = w == pid && WIFEXITED(status);
+  if (exited && WEXITSTATUS(status) == 127) {  // (execve failed: no helper in this environment)
+    *unavailable = true;
+    return "cannot start " + helper;
+  }
+  // (w < 0, ECHILD: a host that ignores SIGCHLD reaped it; the files decide)
+  const bool ok = (exited && WEXITSTATUS(status) == 0) || (w < 0 && errno == ECHILD && !lowered.empty());
+  if (!ok || code.empty() || lowered.empty()) {
+    std::string why = exited ? "exit " + std::to_string(WEXITSTATUS(status))
+                             : (w == pid && WIFSIGNALED(status) ? "signal " + std::to_string(WTERMSIG(status)) : "lost");
+    return "compile process " + why + ": " + logtxt;
+  }
+  sc->code.assign(code.begin(), code.end());
+  sc->lowered = lowered;
+  return std::string();
+}
+
+// Keys being compiled right now (one compile per key; other threads wait).
+std::set<std::string> g_compiling;
+std::condition_variable g_compile_cv;
+
+// Compile the code object for `key` into g_spec_code (no device needed): in
+// the helper process, or in process under g_rtc_mu. Takes g_spec_mu for the
+// cache; the caller holds no lock.
 int spec_compile(const SpecKey& sk, double* ms) {
   *ms = 0;
   const std::string key = sk.str();
@@ -936,17 +1059,25 @@ int spec_compile(const SpecKey& sk, double* ms) {
   };
   std::string err;
   {
-    std::lock_guard<std::mutex> l(g_spec_mu);
-    if (g_spec_code.count(key)) return RT_OK;
-    if (failed(&err)) return fail(RT_E_DEVICE, "scene specialisation: " + err);
+    std::unique_lock<std::mutex> l(g_spec_mu);
+    for (;;) {
+      if (g_spec_code.count(key)) return RT_OK;
+      if (failed(&err)) return fail(RT_E_DEVICE, "scene specialisation: " + err);
+      if (!g_compiling.count(key)) break;
+      g_compile_cv.wait(l);  // (another thread compiles it)
+    }
+    g_compiling.insert(key);
   }
-  std::lock_guard<std::mutex> rl(g_rtc_mu);
-  {
-    std::lock_guard<std::mutex> l(g_spec_mu);  // (compiled by another thread meanwhile)
-    if (g_spec_code.count(key)) return RT_OK;
-    if (failed(&err)) return fail(RT_E_DEVICE, "scene specialisation: " + err);
-  }
-  if (!rtc_load()) return bad(g_rtc.err);
+  struct Done {
+    const std::string& k;
+    ~Done() {
+      {
+        std::lock_guard<std::mutex> l(g_spec_mu);
+        g_compiling.erase(k);
+      }
+      g_compile_cv.notify_all();
+    }
+  } done{key};
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<std::string> defs = {"-DRT_SPEC_KMASK=" + std::to_string(sk.kmask),
                                    "-DRT_SPEC_FEAT=" + std::to_string(sk.feat)};
@@ -987,36 +1118,52 @@ int spec_compile(const SpecKey& sk, double* ms) {
   const std::string name = std::string("rt_render_kernel<") + (sk.lds ? "true" : "false") + ", " +
                            (sk.bvh ? "true" : "false") + ", " + (sk.csg ? "true" : "false") + ", " +
                            (sk.quads == SCH_QUADS ? "true" : "false") + ">";
-  const char* name_expr = name.c_str();
-  hiprtcProgram prog;
-  rtc_sync_env();
-  hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
-                                k_jit_names);
-  if (r != HIPRTC_SUCCESS) return bad(std::string("hiprtcCreateProgram: ") + g_rtc.errstr(r));
   SpecCode sc;
   std::string msg;
-  r = g_rtc.add_name(prog, name_expr);
-  if (r == HIPRTC_SUCCESS) r = g_rtc.compile(prog, (int)opts.size(), opts.data());
-  if (r != HIPRTC_SUCCESS) {
-    size_t n = 0;
-    std::string log;
-    if (g_rtc.log_size(prog, &n) == HIPRTC_SUCCESS && n > 1) {
-      log.resize(n);
-      (void)g_rtc.log(prog, &log[0]);
-    }
-    msg = std::string("hiprtcCompileProgram: ") + g_rtc.errstr(r) + "\n" + log;
-  } else {
-    const char* low = nullptr;
-    size_t n = 0;
-    if (g_rtc.lowered(prog, name_expr, &low) != HIPRTC_SUCCESS || !low) msg = "hiprtcGetLoweredName failed";
-    else if (g_rtc.code_size(prog, &n) != HIPRTC_SUCCESS || n == 0) msg = "hiprtcGetCodeSize failed";
-    else {
-      sc.lowered = low;
-      sc.code.resize(n);
-      if (g_rtc.code(prog, sc.code.data()) != HIPRTC_SUCCESS) msg = "hiprtcGetCode failed";
+  bool compiled = false;
+  const std::string helper = spec_helper();
+  if (!helper.empty()) {
+    bool unavailable = false;
+    msg = spec_compile_child(helper, opts, name, &sc, &unavailable);
+    if (unavailable) {  // the in-process compiler from now on
+      if (!g_helper_off.exchange(1)) fprintf(stderr, "librtamd: compile helper unusable (%s): compiling in process\n", msg.c_str());
+      msg.clear();
+    } else {
+      compiled = true;
     }
   }
-  (void)g_rtc.destroy(&prog);
+  if (!compiled) {
+    std::lock_guard<std::mutex> rl(g_rtc_mu);
+    if (!rtc_load()) return bad(g_rtc.err);
+    const char* name_expr = name.c_str();
+    hiprtcProgram prog;
+    rtc_sync_env();
+    hiprtcResult r = g_rtc.create(&prog, "#include \"rt_render.h\"\n", "rt_spec.hip", k_jit_nsrc, k_jit_srcs,
+                                  k_jit_names);
+    if (r != HIPRTC_SUCCESS) return bad(std::string("hiprtcCreateProgram: ") + g_rtc.errstr(r));
+    r = g_rtc.add_name(prog, name_expr);
+    if (r == HIPRTC_SUCCESS) r = g_rtc.compile(prog, (int)opts.size(), opts.data());
+    if (r != HIPRTC_SUCCESS) {
+      size_t n = 0;
+      std::string log;
+      if (g_rtc.log_size(prog, &n) == HIPRTC_SUCCESS && n > 1) {
+        log.resize(n);
+        (void)g_rtc.log(prog, &log[0]);
+      }
+      msg = std::string("hiprtcCompileProgram: ") + g_rtc.errstr(r) + "\n" + log;
+    } else {
+      const char* low = nullptr;
+      size_t n = 0;
+      if (g_rtc.lowered(prog, name_expr, &low) != HIPRTC_SUCCESS || !low) msg = "hiprtcGetLoweredName failed";
+      else if (g_rtc.code_size(prog, &n) != HIPRTC_SUCCESS || n == 0) msg = "hiprtcGetCodeSize failed";
+      else {
+        sc.lowered = low;
+        sc.code.resize(n);
+        if (g_rtc.code(prog, sc.code.data()) != HIPRTC_SUCCESS) msg = "hiprtcGetCode failed";
+      }
+    }
+    (void)g_rtc.destroy(&prog);
+  }
   if (!msg.empty()) return bad(msg);
   {
     std::lock_guard<std::mutex> l(g_spec_mu);
@@ -1042,7 +1189,7 @@ enum { SPEC_PENDING = 1 };  // internal status of spec_build: queued or compilin
 
 std::vector<SpecKey> g_job_q;  // FIFO of keys to compile; guarded by g_spec_mu
 std::condition_variable g_job_cv;
-std::thread* g_worker = nullptr;
+std::vector<std::thread*> g_workers;  // up to 3 (compiles run in helper processes, so they can overlap)
 bool g_worker_stop = false;
 
 void spec_worker() {
@@ -1073,16 +1220,17 @@ void spec_worker_exit() {
     g_worker_stop = true;
   }
   g_job_cv.notify_all();
-  if (g_worker && g_worker->joinable()) g_worker->join();
+  for (std::thread* t : g_workers)
+    if (t->joinable()) t->join();
 }
 
 // Queue `sk` (caller holds g_spec_mu; the key is not compiled and not queued).
 void spec_enqueue(const SpecKey& sk) {
   g_jobs[sk.str()] = SpecJob();
   g_job_q.push_back(sk);
-  if (!g_worker) {
-    g_worker = new std::thread(spec_worker);
-    std::atexit(spec_worker_exit);
+  if (g_workers.size() < 3) {
+    if (g_workers.empty()) std::atexit(spec_worker_exit);
+    g_workers.push_back(new std::thread(spec_worker));
   }
   g_job_cv.notify_one();
 }
@@ -1261,6 +1409,48 @@ int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile
   sk.nlights = nlights;
   double ms = 0;
   int rc = spec_compile(sk, &ms);
+  if (compile_ms) *compile_ms = ms;
+  return rc;
+}
+
+int rt_debug_spec_compile(const char* key, double* compile_ms) {
+  if (compile_ms) *compile_ms = 0;
+  if (!key) return fail(RT_E_INVALID, "rt_debug_spec_compile: NULL key");
+  std::vector<std::string> f;
+  std::string cur;
+  for (const char* q = key;; q++) {
+    if (*q == ':' || *q == 0) {
+      f.push_back(cur);
+      cur.clear();
+      if (!*q) break;
+    } else {
+      cur += *q;
+    }
+  }
+  if (f.size() != 13) return fail(RT_E_INVALID, "rt_debug_spec_compile: 13 fields expected");
+  SpecKey sk;
+  try {
+    sk.lds = std::stoi(f[0]);
+    sk.bvh = std::stoi(f[1]);
+    sk.csg = std::stoi(f[2]);
+    sk.nobj = std::stoi(f[3]);
+    sk.kinds = f[4];
+    sk.kmask = std::stoi(f[5]);
+    sk.feat = std::stoi(f[6]);
+    sk.nlights = std::stoi(f[7]);
+    sk.pow_bits = std::stoi(f[8]);
+    sk.nocull = std::stoi(f[9]);
+    sk.quads = std::stoi(f[10]);
+    sk.share = std::stoi(f[11]);
+    sk.far = std::stoi(f[12]);
+  } catch (...) {
+    return fail(RT_E_INVALID, "rt_debug_spec_compile: malformed key");
+  }
+  if (sk.quads < SCH_SERIAL || sk.quads > SCH_PAIRS || sk.share < RT_SHARE_OFF || sk.share > RT_SHARE_DEVICE ||
+      sk.nlights < 0 || sk.nlights > SPEC_MAX_LIGHTS || sk.nobj < 0 || sk.nobj > SPEC_MAX_OBJ)
+    return fail(RT_E_INVALID, "rt_debug_spec_compile: field out of range");
+  double ms = 0;
+  const int rc = spec_compile(sk, &ms);
   if (compile_ms) *compile_ms = ms;
   return rc;
 }

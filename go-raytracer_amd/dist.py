@@ -177,7 +177,7 @@ class DistributedRenderer:
     F = 1 is the serial schedule on the caller's current stream."""
 
     def __init__(self, ctx, packed, rank, world, device, mode="interleaved", band=None, pipeline=False,
-                 streams=None):
+                 streams=None, gather_timing=False):
         import torch
         self.ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx]
         if not self.ctxs:
@@ -226,8 +226,9 @@ class DistributedRenderer:
         self.bufs = [self.buf] + [torch.zeros_like(self.buf) for _ in range(nbufs - 1)]
         self.pending = [None] * nbufs
         self.k = 0
-        # (issue, done) event pairs of completed pipelined gathers (telemetry)
-        self.gather_events = []
+        # (issue, done) event pairs of completed pipelined gathers (telemetry,
+        # opt-in: gather_timing=True, bench.py; gather_ms() empties the list)
+        self.gather_events = [] if gather_timing else None
 
     def has_work(self):
         if self.mode in ("frame", "band"):
@@ -292,6 +293,8 @@ class DistributedRenderer:
         """Mean per-frame cost of the completed pipelined gathers to this rank
         (ms from its render end to the collective's completion; None if no
         timed gather ran); resets the record. Call after flush() and a sync."""
+        if self.gather_events is None:
+            return None
         ev, self.gather_events = self.gather_events, []
         if not ev:
             return None

@@ -87,6 +87,8 @@ def load_library(path=None):
     l.rt_render_ex.restype = i
     l.rt_debug_assemble.argtypes = [i, i, i, i, vp, vp]
     l.rt_debug_assemble.restype = i
+    l.rt_debug_spec_compile.argtypes = [C.c_char_p, C.POINTER(C.c_double)]
+    l.rt_debug_spec_compile.restype = i
     if l.rt_abi_version() != abi.RT_ABI_VERSION:
         raise RenderError("librtamd ABI version mismatch")
     _lib = l
@@ -173,7 +175,11 @@ class RenderContext:
 
     def set_work_sharing(self, enable=True):
         """Work sharing at the tail of a launch (specialised kernel only;
-        default off; identical pixels and counters). Applies at once."""
+        identical pixels and counters; applies at once). True / 1 the
+        workgroup board (RT_SHARE_GROUP), 2 the device-wide one
+        (RT_SHARE_DEVICE); the library default is RT_SHARE_AUTO: the device
+        board for CSG scenes at depth >= 7 on strong-scaling shares or without
+        frames in flight, else off."""
         # True / 1: the workgroup board; 2 (abi.RT_SHARE_DEVICE): device-wide
         mode = int(enable)
         _check(self.lib.rt_set_work_sharing(self.handle, mode), "rt_set_work_sharing")

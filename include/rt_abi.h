@@ -446,6 +446,14 @@ int rt_specialized(rt_context *ctx, int *active, double *compile_ms);
                                         lights is specialised (0: the generic light loop) */
 int rt_spec_precompile(int nobj, const int *kinds, int features, double *compile_ms);
 
+/* Diagnostic (tests, no device): compile the specialised variant named by
+ * the library's internal key "lds:bvh:csg:nobj:kinds:kmask:feat:nlights:
+ * pow_bits:nocull:schedule:share:far" (schedule 0 serial, 1 quads, 2 pairs;
+ * share an RT_SHARE_* mode) exactly as a launch would ask for it. Every
+ * compile runs in the helper process csrc/rt_spec_cc (RT_SPEC_INPROC=1: in
+ * this process), so a compiler abort is a failed compile, not a dead caller. */
+int rt_debug_spec_compile(const char *key, double *compile_ms);
+
 /* Diagnostic (tests): run surface program `program` of the context's scene on
  * n (face, u, v) inputs on the device; out10 receives n x 10 Material fields
  * (rt_material order), err n flags (1 = the reference would raise). */
