@@ -2700,9 +2700,11 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
                 (double)pd[1] / std::max(1ull, pd[0]), pd[2], (double)pd[3] / std::max(1ull, pd[2]), pd[4],
                 (double)pd[5] / std::max(1ull, pd[4]));
       }
-      fprintf(stderr, "[waves] lifetime mean %.4g cycles, max %.4g cycles (mean/max %.3f)\n",
-              (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches), (double)bd[7],
-              (double)bd[6] / std::max(1.0, (double)c->last_waves * c->launches) / (double)std::max(1ull, bd[7]));
+      unsigned long long steps = 0;
+      HIP_TRY(hipMemcpy(&steps, c->stats + ST_CLOCKSTEP, sizeof steps, hipMemcpyDeviceToHost));
+      const double nw = std::max(1.0, (double)c->last_waves * c->launches - (double)steps);
+      fprintf(stderr, "[waves] lifetime mean %.4g cycles, max %.4g cycles (mean/max %.3f; %llu waves with a clock step left out)\n",
+              (double)bd[6] / nw, (double)bd[7], (double)bd[6] / nw / (double)std::max(1ull, bd[7]), steps);
       if (bd[4] + bd[5])
         fprintf(stderr, "[bvh] wave traversals trace=%llu shadow=%llu; nodes/traversal trace=%.1f shadow=%.1f; "
                         "leaves/traversal trace=%.1f shadow=%.1f\n", bd[4], bd[5], (double)bd[0] / (double)std::max(1ull, bd[4]),

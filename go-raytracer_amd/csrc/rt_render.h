@@ -178,7 +178,7 @@ enum { QSET = QHEADS * QSTRIDE /* u32 per launch set of heads */,
 enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
        ST_PHASE = 16, N_PHASE = 10, ST_BVHDIAG = 26, ST_EXDIAG = 34, ST_SHDIAG = 48, ST_PASSDIAG = 54,
-       ST_WATCHDOG = 63,
+       ST_CLOCKSTEP = 60, ST_WATCHDOG = 63,
        STATS_PART = 16 /* u64 per workgroup record: one 128-B line */ };
 // Diagnostic build (RT_PHASE_TIMING): work-sharing events, ST_SHDIAG + k:
 // 0 samples posted, 1 subtrees posted, 2 claims, 3 reclaims, 4 waits, 5 rounds
@@ -1598,15 +1598,42 @@ __device__ __forceinline__ void gs_st(uint64_t* p, uint64_t v) { __hip_atomic_st
 __device__ __forceinline__ unsigned int gs_ld32(unsigned int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, RT_AG_SCOPE);
 }
-// every store this lane issued has completed (before a publishing store)
+// Ordering. Publication is release / acquire by construction, without the
+// L2 writeback / invalidate the compiler emits for agent-scope release /
+// acquire on ordinary memory (buffer_wbl2 / buffer_inv: an agent-scope fence
+// per sample cost round 3's sample-unit experiment 41 ms), which the board
+// does not need: it is uncached (MTYPE UC), so no L2 of any XCD holds a line
+// of it, and every access reaches memory.
+//   * release (gs_drain before the publishing store -- POSTED, DONE, the
+//     ticket): s_waitcnt vmcnt(0) waits until every earlier store of the lane
+//     has been acknowledged by memory, and its "memory" clobber stops the
+//     compiler moving any memory operation across it;
+//   * acquire (gs_acquire after the load or CAS that observed POSTED / DONE,
+//     before the payload loads): the same wait -- the observing access has
+//     returned before any later load issues -- and the same compiler barrier,
+//     so no payload load is hoisted above the observation.
+// Every shared word is still accessed with agent-scope atomics (no tearing,
+// past the CU's L1).
 __device__ __forceinline__ void gs_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void gs_acquire() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ bool gs_cas(uint64_t* p, uint64_t from, uint64_t to) {
   return __hip_atomic_compare_exchange_strong(p, &from, to, __ATOMIC_RELAXED, __ATOMIC_RELAXED, RT_AG_SCOPE);
+}
+// the claim: CAS POSTED -> CLAIMED, then (acquire) the slot's payload may be read
+__device__ __forceinline__ bool gs_claim(uint64_t* r) {
+  const bool ok = gs_cas(r + 7, GS_POSTED, GS_CLAIMED);
+  gs_acquire();
+  return ok;
 }
 __device__ __forceinline__ uint64_t* gs_slot(uint64_t* board, int q) { return board + (size_t)q * GS_REC; }
 // owner: take back a slot nobody claimed
 __device__ __forceinline__ bool gs_reclaim(uint64_t* board, int q) { return gs_cas(gs_slot(board, q) + 7, GS_POSTED, GS_FREE); }
-__device__ __forceinline__ bool gs_done(uint64_t* board, int q) { return gs_ld(gs_slot(board, q) + 7) == GS_DONE; }
+// owner: has the helper delivered? (acquire: gs_take's colour loads follow)
+__device__ __forceinline__ bool gs_done(uint64_t* board, int q) {
+  const bool d = gs_ld(gs_slot(board, q) + 7) == GS_DONE;
+  gs_acquire();
+  return d;
+}
 // owner: the delivered colour (after gs_done); the slot is free again
 __device__ __forceinline__ d3 gs_take(uint64_t* board, int q) {
   uint64_t* r = gs_slot(board, q);
@@ -2607,7 +2634,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
             if ((uint32_t)(e >> 32) == (uint32_t)t && (uint32_t)e < P.gslots) {
               const int q = (int)(uint32_t)e;
               uint64_t* r = gs_slot(P.gboard, q);
-              if (gs_cas(r + 7, GS_POSTED, GS_CLAIMED)) {  // (else its owner took it back)
+              if (gs_claim(r)) {  // (else its owner took it back)
                 SHDIAG(SH_CLAIM);
                 ray.o = mk(__longlong_as_double((long long)gs_ld(r + 0)), __longlong_as_double((long long)gs_ld(r + 1)),
                            __longlong_as_double((long long)gs_ld(r + 2)));
@@ -3828,10 +3855,19 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     atomicAdd(P.stats + ST_PASSDIAG + 3, (unsigned long long)pd_shl);
     atomicAdd(P.stats + ST_PASSDIAG + 4, (unsigned long long)pd_gen);
     atomicAdd(P.stats + ST_PASSDIAG + 5, (unsigned long long)pd_genl);
-    // wave lifetimes (main loop): mean vs max shows the load imbalance
-    const uint64_t life = stamp() - life_t0;
-    atomicAdd(P.stats + ST_BVHDIAG + 6, (unsigned long long)life);
-    atomicMax(P.stats + ST_BVHDIAG + 7, (unsigned long long)life);
+    // wave lifetimes (main loop): mean vs max shows the load imbalance. A
+    // wave whose end stamp reads below its start (the shader clock stepped
+    // back under it: round 5 saw 1.8e19-cycle "lifetimes" in the first launch
+    // of a run) is counted in ST_CLOCKSTEP and left out of the mean and max.
+    const uint64_t t_end = stamp();
+    const bool clock_ok = t_end >= life_t0;
+    const uint64_t life = clock_ok ? t_end - life_t0 : 0;
+    if (clock_ok) {
+      atomicAdd(P.stats + ST_BVHDIAG + 6, (unsigned long long)life);
+      atomicMax(P.stats + ST_BVHDIAG + 7, (unsigned long long)life);
+    } else {
+      atomicAdd(P.stats + ST_CLOCKSTEP, 1ull);
+    }
     if (P.wdiag) {
       P.wdiag[(size_t)wslot * 4 + 0] = life;
       P.wdiag[(size_t)wslot * 4 + 1] = nchunk_taken;

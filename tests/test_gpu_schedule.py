@@ -5,11 +5,15 @@ and launches on several streams. None of them may change a byte or a
 counter: every case is checked against the CPU oracle (raytracer.go:589-682
 restated, tests/oracle_bind.py).
 """
+import os
+
 import numpy as np
 import pytest
 
 import go_raytracer_amd as rt
 import oracle_bind
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -244,3 +248,59 @@ def test_device_sharing_full_c4csg_frame_and_shares():
     finally:
         a.close()
         b.close()
+
+
+BOARD_STRESS = r'''
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+from __graft_entry__ import load_package
+import oracle_bind
+rt = load_package()
+packed = rt.scene.convert(rt.configs.c4csg())
+ref, ost = oracle_bind.render_rows(packed, threads=16)
+c = rt.RenderContext(0, specialize=True)
+c.set_work_sharing(rt.abi.RT_SHARE_DEVICE)
+c.set_scene(packed)
+assert c.scene_info() & rt.abi.RT_INFO_SHARE_DEVICE
+c.read_stats(reset=True)
+img = c.render()
+st = c.read_stats(reset=True)
+bad = int((img != ref).any(axis=-1).sum())
+print("whole frame: %%d pixels differ, counters %%s" %% (bad, "equal" if st.as_dict() == ost.as_dict() else "DIFFER"))
+ok = bad == 0 and st.as_dict() == ost.as_dict()
+world = 8
+nt, K = rt.dist.tile_rows(packed.height, world)
+tot = rt.abi.rt_stats()
+for r in range(world):
+    n = max(0, min(K, (nt - r + world - 1) // world))
+    buf = torch.zeros((n * 8, packed.width, 4), dtype=torch.uint8, device="cuda:0")
+    c.render_tile_rows_async(r, world, n, buf)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    for j in range(n):
+        t = r + j * world
+        y0, y1 = t * 8, min(packed.height, t * 8 + 8)
+        if not np.array_equal(got[j * 8:j * 8 + (y1 - y0)], ref[y0:y1]):
+            ok = False
+            print("share %%d tile row %%d differs" %% (r, t))
+st = c.read_stats(reset=True)
+ok = ok and st.as_dict() == ost.as_dict()
+print("shares: counters %%s" %% ("equal" if st.as_dict() == ost.as_dict() else "DIFFER"))
+print("board stress ok" if ok else "board stress MISMATCH")
+''' % (ROOT, os.path.join(ROOT, "tests"))
+
+
+def test_device_board_stress_against_oracle():
+    """The device-wide board at its most contended: every drained wave of the
+    device stays as a helper (RT_GS_HELPERS far above the wave count) and busy
+    waves poll the board every round (RT_GS_POLL 0) -- the full 4K c4csg
+    frame and its 8 interleaved shares against the CPU oracle, bytes and
+    counters (in a fresh process, so that the stress flags compile)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, RT_SPEC_EXTRA_FLAGS="-DRT_GS_HELPERS=1000000 -DRT_GS_POLL=0")
+    r = subprocess.run([sys.executable, "-c", BOARD_STRESS], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "board stress ok" in r.stdout, r.stdout + r.stderr
