@@ -1371,11 +1371,14 @@ __device__ __forceinline__ uint64_t stamp() {
   return t;
 }
 #define PH_BEGIN() uint64_t ph_t0_ = stamp()
-#define PH_MARK(k)              \
-  do {                          \
-    uint64_t t_ = stamp();      \
-    ph_acc[k] += t_ - ph_t0_;   \
-    ph_t0_ = t_;                \
+// (the asm comment names the phase that ends here in the ISA listing:
+// scripts/isa_phases.py splits the diagnostic kernel's code at these marks)
+#define PH_MARK(k)                        \
+  do {                                    \
+    uint64_t t_ = stamp();                \
+    asm volatile("; @phase_end " #k ::: "memory"); \
+    ph_acc[k] += t_ - ph_t0_;             \
+    ph_t0_ = t_;                          \
   } while (0)
 #else
 #define PH_BEGIN() (void)0
