@@ -2699,6 +2699,10 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
         fprintf(stderr, "[passes] trace %llu (%.1f lanes), shade %llu (%.1f lanes), gen %llu (%.1f lanes)\n", pd[0],
                 (double)pd[1] / std::max(1ull, pd[0]), pd[2], (double)pd[3] / std::max(1ull, pd[2]), pd[4],
                 (double)pd[5] / std::max(1ull, pd[4]));
+        unsigned long long ld[2];
+        HIP_TRY(hipMemcpy(ld, c->stats + ST_LANEDIAG, sizeof ld, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[lanes] rounds %llu, lanes waiting in S_DONE (finished quad / pair samples) %.2f per round\n", ld[1],
+                (double)ld[0] / (double)std::max(1ull, ld[1]));
       }
       unsigned long long steps = 0;
       HIP_TRY(hipMemcpy(&steps, c->stats + ST_CLOCKSTEP, sizeof steps, hipMemcpyDeviceToHost));

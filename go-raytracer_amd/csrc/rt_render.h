@@ -178,7 +178,8 @@ enum { QSET = QHEADS * QSTRIDE /* u32 per launch set of heads */,
 enum { SCH = 32 };  // objects per stream chunk (RT_STREAM): SCH * GEO * 8 B + SCH * 4 B per wave
 enum { ST_SHADOW = 0, ST_TRACED = 1, ST_SHADED = 2, ST_SURFERR = 3, ST_STESTS = 4, ST_COUNT = ST_STESTS + RT_NUM_KINDS,
        ST_PHASE = 16, N_PHASE = 10, ST_BVHDIAG = 26, ST_EXDIAG = 34, ST_SHDIAG = 48, ST_PASSDIAG = 54,
-       ST_CLOCKSTEP = 60, ST_WATCHDOG = 63,
+       ST_CLOCKSTEP = 60, ST_LANEDIAG = 61 /* 61: lanes waiting in S_DONE, summed over rounds; 62: rounds */,
+       ST_WATCHDOG = 63,
        STATS_PART = 16 /* u64 per workgroup record: one 128-B line */ };
 // Diagnostic build (RT_PHASE_TIMING): work-sharing events, ST_SHDIAG + k:
 // 0 samples posted, 1 subtrees posted, 2 claims, 3 reclaims, 4 waits, 5 rounds
@@ -2097,6 +2098,7 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
   uint64_t bd_tnodes = 0, bd_snodes = 0, bd_tleaf = 0, bd_sleaf = 0, bd_trays = 0, bd_srays = 0;
   // passes and their working lanes: TRACE (tracing lanes), SHADE (hit lanes), gen (new sample rays)
   uint64_t pd_tr = 0, pd_trl = 0, pd_sh = 0, pd_shl = 0, pd_gen = 0, pd_genl = 0;
+  uint64_t ld_done = 0, ld_rounds = 0;  // lanes holding a finished quad / pair sample (S_DONE) per round
 #ifdef RT_COST_MAP
   uint32_t lane_cost = 0;  // node visits charged to this lane's pixel (diagnostic)
 #endif
@@ -2845,6 +2847,10 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     } else {
       if (!wave_any(state != S_IDLE)) break;
     }
+#ifdef RT_PHASE_TIMING
+    ld_done += (uint64_t)__popcll(wave_ballot(state == S_DONE));
+    ld_rounds++;
+#endif
     PH_MARK(0);
     // ---- new sample rays for every lane that needs one, in one block ----
     if (wave_any(need_gen)) {
@@ -3858,6 +3864,8 @@ __global__ __launch_bounds__(WG, RT_MIN_WAVES) void rt_render_kernel(const char*
     atomicAdd(P.stats + ST_PASSDIAG + 3, (unsigned long long)pd_shl);
     atomicAdd(P.stats + ST_PASSDIAG + 4, (unsigned long long)pd_gen);
     atomicAdd(P.stats + ST_PASSDIAG + 5, (unsigned long long)pd_genl);
+    atomicAdd(P.stats + ST_LANEDIAG + 0, (unsigned long long)ld_done);
+    atomicAdd(P.stats + ST_LANEDIAG + 1, (unsigned long long)ld_rounds);
     // wave lifetimes (main loop): mean vs max shows the load imbalance. A
     // wave whose end stamp reads below its start (the shader clock stepped
     // back under it: round 5 saw 1.8e19-cycle "lifetimes" in the first launch
