@@ -106,6 +106,38 @@ const std::array<const void*, 16> k_kernels = kernel_table(std::make_integer_seq
 // ===========================================================================
 namespace {
 
+// The process environment as it was when this library loaded. Python's
+// os.environ (putenv / unsetenv) reallocates the environment array and frees
+// the strings it replaces while this library's calls run without the GIL
+// (ctypes releases it), and glibc's getenv takes no lock, so reading
+// `environ` or calling getenv during a call can touch freed memory: the
+// environment-race GPU test (tests/test_gpu_render_ex.py) segfaulted that way
+// once in round 6, in the per-call band-plan lookup. The library reads its
+// knobs (rt_getenv), and gives the compile helper and the in-process
+// compiler's namespace, this load-time copy only; environment changes made
+// after the library is loaded do not reach it (set RT_* knobs before loading).
+struct EnvSnap {
+  std::vector<std::string> s;
+  std::vector<char*> p;  // execve-style array into s
+};
+EnvSnap* env_snap() {
+  static EnvSnap* e = [] {
+    EnvSnap* x = new EnvSnap;  // (never freed: pointers into it are handed out)
+    for (char** v = environ; v && *v; ++v) x->s.emplace_back(*v);
+    for (auto& t : x->s) x->p.push_back(&t[0]);
+    x->p.push_back(nullptr);
+    return x;
+  }();
+  return e;
+}
+__attribute__((constructor)) void env_snap_at_load() { (void)env_snap(); }
+const char* rt_getenv(const char* name) {
+  const size_t n = strlen(name);
+  for (const std::string& t : env_snap()->s)
+    if (t.size() > n && t[n] == '=' && t.compare(0, n, name) == 0) return t.c_str() + n + 1;
+  return nullptr;
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -671,8 +703,8 @@ bool rtc_load() {
   if (g_rtc.tried) return g_rtc.create != nullptr;
   g_rtc.tried = true;
   std::string path;
-  if (const char* e = getenv("RT_HIPRTC_LIB")) path = e;
-  else path = std::string(getenv("ROCM_PATH") ? getenv("ROCM_PATH") : "/opt/rocm") + "/lib/libhiprtc.so.7";
+  if (const char* e = rt_getenv("RT_HIPRTC_LIB")) path = e;
+  else path = std::string(rt_getenv("ROCM_PATH") ? rt_getenv("ROCM_PATH") : "/opt/rocm") + "/lib/libhiprtc.so.7";
   void* h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
   if (!h) {
     const char* de = dlerror();
@@ -704,7 +736,8 @@ bool rtc_load() {
   // environment array and free the old one, so the private copy can dangle,
   // and the compiler reading its environment then crashed the process (a
   // segfault inside rt_set_scene, seen once in a full GPU test run).
-  // rtc_sync_env gives it a library-owned copy before every compile.
+  // rtc_sync_env points it at the library's load-time copy before every
+  // compile.
   Lmid_t lm;
   if (dlinfo(h, RTLD_DI_LMID, &lm) == 0) {
     if (void* lc = dlmopen(lm, "libc.so.6", RTLD_NOW | RTLD_NOLOAD)) {
@@ -716,28 +749,12 @@ bool rtc_load() {
   return true;
 }
 
-// The namespace's environment: a deep copy of the host's, owned by the
-// library and never freed (a compile runs for seconds while another host
-// thread may setenv, and the compiler may keep pointers getenv gave it). An
-// unchanged environment reuses the last copy. Caller holds g_rtc_mu.
-struct EnvCopy {
-  std::vector<std::string> s;
-  std::vector<char*> p;
-};
-std::vector<EnvCopy*> g_env_copies;
-
+// The namespace's environment: the library's load-time copy (env_snap),
+// owned by the library and never freed or changed, so neither a host thread's
+// setenv nor a compile that keeps pointers getenv gave it can see it move.
+// Caller holds g_rtc_mu.
 void rtc_sync_env() {
-  if (!g_rtc.env) return;
-  std::vector<std::string> cur;
-  for (char** e = environ; e && *e; ++e) cur.emplace_back(*e);
-  if (g_env_copies.empty() || g_env_copies.back()->s != cur) {
-    EnvCopy* c = new EnvCopy;
-    c->s.swap(cur);
-    for (auto& x : c->s) c->p.push_back(&x[0]);
-    c->p.push_back(nullptr);
-    g_env_copies.push_back(c);
-  }
-  *g_rtc.env = g_env_copies.back()->p.data();
+  if (g_rtc.env) *g_rtc.env = env_snap()->p.data();
 }
 
 
@@ -839,7 +856,7 @@ void csg_mask_program(const int* code, int len, std::vector<int>& out) {
 // environment at process start (experiments).
 bool scene_in_lds(const DevScene& s);
 bool use_quads(int sched, const DevScene& s, uint64_t pixels, int cus, int inflight) {
-  static const int env = getenv("RT_PIXEL_QUADS") ? atoi(getenv("RT_PIXEL_QUADS")) : -1;
+  static const int env = rt_getenv("RT_PIXEL_QUADS") ? atoi(rt_getenv("RT_PIXEL_QUADS")) : -1;
   if (env >= 0) return env != 0;
   if (sched == RT_SCHED_PIXEL) return false;
   if (sched == RT_SCHED_QUADS) return true;
@@ -878,9 +895,9 @@ int pick_share(int mode, const DevScene& s, uint64_t pixels, int cus, int inflig
 }
 
 int pick_schedule(int sched, const DevScene& s, uint64_t pixels, int cus, int inflight, bool spec) {
-  static const int env = getenv("RT_PIXEL_PAIRS") ? atoi(getenv("RT_PIXEL_PAIRS")) : -1;
+  static const int env = rt_getenv("RT_PIXEL_PAIRS") ? atoi(rt_getenv("RT_PIXEL_PAIRS")) : -1;
   if (env > 0 || sched == RT_SCHED_PAIRS) return SCH_PAIRS;
-  static const int qenv = getenv("RT_PIXEL_QUADS") ? atoi(getenv("RT_PIXEL_QUADS")) : -1;
+  static const int qenv = rt_getenv("RT_PIXEL_QUADS") ? atoi(rt_getenv("RT_PIXEL_QUADS")) : -1;
   if (sched == RT_SCHED_AUTO && qenv < 0 && env < 0 && spec && inflight > 1 && scene_in_lds(s) && !s.has_csg &&
       s.branching) {
     const double ppl = (double)pixels / ((double)std::max(1, cus) * 4 * 3 * 64);  // pixels per lane
@@ -891,7 +908,7 @@ int pick_schedule(int sched, const DevScene& s, uint64_t pixels, int cus, int in
 }
 
 bool scene_in_lds(const DevScene& s) {
-  static const bool force_global = getenv("RT_SCENE_GLOBAL") && atoi(getenv("RT_SCENE_GLOBAL")) != 0;
+  static const bool force_global = rt_getenv("RT_SCENE_GLOBAL") && atoi(rt_getenv("RT_SCENE_GLOBAL")) != 0;
   return !force_global && s.blob_bytes <= (int)LDS_MAX_BYTES;
 }
 
@@ -937,7 +954,7 @@ std::string spec_helper() {
       if (access(p.c_str(), X_OK) == 0) path = p;
     }
   });
-  const char* e = getenv("RT_SPEC_INPROC");
+  const char* e = rt_getenv("RT_SPEC_INPROC");
   if ((e && atoi(e) != 0) || g_helper_off.load()) return std::string();
   return path;
 }
@@ -949,7 +966,7 @@ std::string spec_helper() {
 std::string spec_compile_child(const std::string& helper, const std::vector<const char*>& opts, const std::string& name,
                                SpecCode* sc, bool* unavailable) {
   *unavailable = false;
-  const char* td = getenv("TMPDIR");
+  const char* td = rt_getenv("TMPDIR");
   std::string tmpl = std::string(td && *td ? td : "/tmp") + "/rt_spec_XXXXXX";
   std::vector<char> dbuf(tmpl.begin(), tmpl.end());
   dbuf.push_back(0);
@@ -961,11 +978,7 @@ std::string spec_compile_child(const std::string& helper, const std::vector<cons
   std::vector<const char*> argv = {helper.c_str(), out.c_str(), name.c_str()};
   argv.insert(argv.end(), opts.begin(), opts.end());
   argv.push_back(nullptr);
-  std::vector<std::string> envs;  // a snapshot of the environment for the child
-  for (char** e = environ; e && *e; ++e) envs.emplace_back(*e);
-  std::vector<char*> envp;
-  for (auto& x : envs) envp.push_back(&x[0]);
-  envp.push_back(nullptr);
+  char* const* envp = env_snap()->p.data();  // the child's environment: the load-time copy
   auto cleanup = [&] {
     unlink(out.c_str());
     unlink(outname.c_str());
@@ -985,7 +998,7 @@ std::string spec_compile_child(const std::string& helper, const std::vector<cons
     if (syscall(SYS_close_range, 3u, ~0u, 0u) != 0)
 #endif
       for (int fd = 3; fd < 4096; fd++) close(fd);
-    execve(helper.c_str(), (char* const*)argv.data(), envp.data());
+    execve(helper.c_str(), (char* const*)argv.data(), envp);
     _exit(127);
   }
   if (lfd >= 0) close(lfd);
@@ -1101,7 +1114,7 @@ int spec_compile(const SpecKey& sk, double* ms) {
 #else
   const char* baked = nullptr;
 #endif
-  for (const char* e : {baked, (const char*)getenv("RT_SPEC_EXTRA_FLAGS")}) {
+  for (const char* e : {baked, (const char*)rt_getenv("RT_SPEC_EXTRA_FLAGS")}) {
     if (!e) continue;
     std::string cur;
     for (const char* q = e;; q++) {
@@ -2253,12 +2266,12 @@ static int order_for(rt_context* c, int y0, int trow0, int stride, int tiles_x, 
   // 9.96-9.99 ms, C3 3.013-3.016 -> 2.991-3.010 ms (an eighth: c4csg 9.94-9.98,
   // C3 3.021-3.026; profiles/r05/order_ab/). RT_ORDER_TOP=d (environment,
   // experiments): the costliest 1/d first, d = 1 sorts all.
-  static const int topd = getenv("RT_ORDER_TOP") ? std::max(1, atoi(getenv("RT_ORDER_TOP"))) : 6;
+  static const int topd = rt_getenv("RT_ORDER_TOP") ? std::max(1, atoi(rt_getenv("RT_ORDER_TOP"))) : 6;
   // RT_ORDER_TAIL=d (experiments): the cheapest 1/d of the tiles go last, in
   // tile order, so waves that run out of work early finish on short tiles.
   // Measured slower: C3 3.53-3.56 vs 3.43 ms, C4 5.25-5.29 vs 5.16 (d = 4, 8,
   // 16), 8-rank shares within 2 % (profiles/r03/order/tail.log): off.
-  static const int taild = getenv("RT_ORDER_TAIL") ? std::max(0, atoi(getenv("RT_ORDER_TAIL"))) : 0;
+  static const int taild = rt_getenv("RT_ORDER_TAIL") ? std::max(0, atoi(rt_getenv("RT_ORDER_TAIL"))) : 0;
   {
     const int top = n / topd;
     const int tail = taild > 0 ? std::min(n - top, n / taild) : 0;
@@ -2321,7 +2334,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // (the brute-force specialised kernel, RT_CULL=0, reads records with scalar
   // loads instead: no stream buffers; tuning builds with RT_SPEC_EXTRA_FLAGS
   // keep the buffers: they may select the LDS stream)
-  static const bool spec_extra = getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
+  static const bool spec_extra = rt_getenv("RT_SPEC_EXTRA_FLAGS") != nullptr;
   const bool use_stream = !lds && !s.use_bvh && !s.has_csg && (spec_extra || !(spec && !(c->accel & RT_ACCEL_CULL)));
   // the generic kernels have no pairs flavour: quads instead (same pixels)
   const bool quads = sch == SCH_QUADS || (sch == SCH_PAIRS && !spec);
@@ -2358,10 +2371,10 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   int lds_levels = plan_hit ? pl.lds_levels : 0, lds_full = plan_hit ? pl.lds_full : 0;
   if (!plan_hit && c->lds_per_cu > 0 && c->lds_per_block > 0) {
     const int avail = std::min(c->lds_per_block, c->lds_per_cu / std::min(per_cu, 8)) - shmem;
-    if (const char* e = getenv("RT_LDS_FULL")) lds_full = std::max(0, std::min(frames, atoi(e)));
+    if (const char* e = rt_getenv("RT_LDS_FULL")) lds_full = std::max(0, std::min(frames, atoi(e)));
     while (lds_full > 0 && lds_full * (ext_bytes + level_bytes) > avail) lds_full--;
     lds_levels = std::max(lds_full, std::min(frames, (avail - lds_full * ext_bytes) / level_bytes));
-    if (const char* e = getenv("RT_LDS_LEVELS")) lds_levels = std::max(lds_full, std::min(lds_levels, atoi(e)));
+    if (const char* e = rt_getenv("RT_LDS_LEVELS")) lds_levels = std::max(lds_full, std::min(lds_levels, atoi(e)));
     while (lds_levels > 0 && occupancy(shmem + lds_levels * level_bytes + lds_full * ext_bytes) < per_cu) {
       lds_levels--;
       lds_full = std::min(lds_full, lds_levels);
@@ -2370,7 +2383,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   if (!plan_hit) pl = LaunchPlan{plan_fn, shmem, frames, per_cu, lds_levels, lds_full};
   const int ext_off = shmem + lds_levels * level_bytes;
   shmem = ext_off + lds_full * ext_bytes;
-  static const bool dbg = getenv("RT_DEBUG_LAUNCH") != nullptr;
+  static const bool dbg = rt_getenv("RT_DEBUG_LAUNCH") != nullptr;
   if (dbg)
     fprintf(stderr, "[launch] blocks/CU %d, LDS/block %d B (fixed %d, frame cores %d levels, full frames %d levels), frames %d\n",
             per_cu, shmem, frames_off, lds_levels, lds_full, frames);
@@ -2461,7 +2474,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
   // estimate: one unit per frame tile; a render: the launch's pixels, its
   // tiles dealt in order of estimated cost
   // (estimate points per tile: RT_EST_PTS=1 in the environment, experiments)
-  static const int est_pts = getenv("RT_EST_PTS") && atoi(getenv("RT_EST_PTS")) == 1 ? 1 : 4;
+  static const int est_pts = rt_getenv("RT_EST_PTS") && atoi(rt_getenv("RT_EST_PTS")) == 1 ? 1 : 4;
   P.est_pts = est_pts;
   size_t slots = est ? (size_t)P.tiles_x * tiles_y * est_pts : (size_t)P.tiles_x * tiles_y * TILE * TILE;
   if (!est) {
@@ -2529,7 +2542,7 @@ static int launch(rt_context* c, int y0, int y1, int trow0, int stride, int ntro
 // a costly estimate. RT_TILE_ORDER=0 / 2 (environment, experiments): never /
 // also for HBM scenes with a BVH.
 static bool want_order(const rt_context* c) {
-  static const int env = getenv("RT_TILE_ORDER") ? atoi(getenv("RT_TILE_ORDER")) : 1;
+  static const int env = rt_getenv("RT_TILE_ORDER") ? atoi(rt_getenv("RT_TILE_ORDER")) : 1;
   const DevScene& s = c->sc;
   return env != 0 && c->order_on && s.nobj > 0 && (scene_in_lds(s) || (env == 2 && s.use_bvh));
 }

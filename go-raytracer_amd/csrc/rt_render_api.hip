@@ -74,7 +74,7 @@ void scene_bytes(const rt_scene* s, std::vector<char>& out) {
 enum { API_CTX = 2, API_MAX_BANDS = 16 };
 
 int env_int(const char* name, int def) {
-  const char* e = getenv(name);
+  const char* e = rt_getenv(name);  // (the load-time copy: rt_kernel.hip env_snap)
   return e ? atoi(e) : def;
 }
 
@@ -115,9 +115,12 @@ struct ApiPlan {
 // 8(e): every device the same mix of sky, floor and glass). Bands per slot:
 // `forced` (> 0), else RT_RENDER_BANDS, else one per ~2 M pixels of the share,
 // at most 4 -- measured on C3 4K with one device (scripts/api_seam.py,
-// profiles/r05/seam/): 1 / 2 / 4 / 8 bands 4.65 / 4.16 / 3.89 / 4.10 ms per
-// call (more bands: a shorter exposed copy of the last band, but each band
-// launch has its own tail).
+// profiles/r05/seam/): 1 / 2 / 4 / 8 equal bands 4.65 / 4.16 / 3.89 / 4.10 ms
+// per call (more bands: a shorter exposed copy of the last band, but each band
+// launch has its own tail). Band sizes decrease (weights 4:3:2:1 for 4 bands;
+// RT_RENDER_BAND_SHAPE=0: equal), so the exposed copy is that of the smallest
+// band: C3 3.83-3.84 -> 3.61-3.72 ms per call, c4csg 12.44 -> 11.45 ms
+// (scripts/gpu/r6_bands.sh, profiles/r06/bands/).
 ApiPlan api_plan(int W, int H, int N, int forced) {
   ApiPlan p;
   p.W = W;
@@ -125,6 +128,7 @@ ApiPlan api_plan(int W, int H, int N, int forced) {
   p.N = N;
   p.trows = (H + TILE - 1) / TILE;
   const int env = env_int("RT_RENDER_BANDS", 0);
+  const int shape = env_int("RT_RENDER_BAND_SHAPE", 1);
   for (int d = 0; d < N; d++) {
     const int n = d < p.trows ? (p.trows - 1 - d) / N + 1 : 0;
     p.ntr.push_back(n);
@@ -133,7 +137,27 @@ ApiPlan api_plan(int W, int H, int N, int forced) {
       const long long px = (long long)n * TILE * W;
       int nb = forced > 0 ? forced : env > 0 ? env : (int)std::min<long long>(4, std::max<long long>(1, (px + (1 << 20)) / (2 << 20)));
       nb = std::max(1, std::min({nb, (int)API_MAX_BANDS, n}));
-      for (int k = 0; k <= nb; k++) b.push_back((int)((long long)n * k / nb));
+      if (shape == 1 && nb > 1) {
+        // decreasing bands (weights nb, nb-1, ..., 1): the last band, whose
+        // copy is the exposed tail, is the smallest
+        const long long tot = (long long)nb * (nb + 1) / 2;
+        long long acc = 0;
+        b.push_back(0);
+        for (int k = 0; k < nb; k++) {
+          acc += nb - k;
+          const int e = (int)(n * acc / tot);
+          b.push_back(std::max(e, b.back() + 1));
+        }
+        b.back() = n;
+        bool ok = true;  // (tiny shares: equal bands)
+        for (size_t k = 1; k < b.size(); k++) ok = ok && b[k] > b[k - 1];
+        if (!ok) {
+          b.clear();
+          for (int k = 0; k <= nb; k++) b.push_back((int)((long long)n * k / nb));
+        }
+      } else {
+        for (int k = 0; k <= nb; k++) b.push_back((int)((long long)n * k / nb));
+      }
     }
     p.bounds.push_back(b);
   }

@@ -56,13 +56,15 @@ def test_rt_render_scene_reuse_and_in_place_change():
 
 
 @pytest.mark.parametrize("bands", [1, 2, 3, 7])
-def test_rt_render_row_bands_equal_oracle(bands, monkeypatch):
+def test_rt_render_row_bands_equal_oracle(bands):
     """The frame rendered as 1..7 row bands alternating over the two contexts
-    (ragged last band) equals the oracle, counters summed exactly."""
-    monkeypatch.setenv("RT_RENDER_BANDS", str(bands))
+    (ragged last band; bands of decreasing size, the default plan) equals the
+    oracle, counters summed exactly. (The band count comes through
+    rt_render_opts.bands: the library reads RT_* knobs from its load-time copy
+    of the environment only.)"""
     p = rt.scene.convert(rt.configs.c4(width=77, height=53))
     ref, ost = oracle_bind.render_rows(p)
-    out, st, tm = call(p)
+    out, st, tm = rt.render_frame(p, bands=bands)
     assert tm.bands == min(bands, (53 + 7) // 8)
     assert np.array_equal(out, ref)
     assert st.as_dict() == ost.as_dict()

