@@ -13,4 +13,4 @@ for c in ${INFLIGHT_CFGS:-c3 c3cone c4 c2 c4csg c5}; do
 import json; d=json.load(open('$O/strong/inflight_$c.json'))
 print('$c', ' '.join('w%d: %.3f/%s' % (w, d['w%d_f2_max_ms' % w], d.get('w%d_f2_eff_max' % w)) for w in (1, 2, 4, 8)))"
 done
-if [ -z "$NO_BRUTE" ]; then bash scripts/gpu/brute_pmc.sh r5final > $O/brute.log 2>&1 || { tail -5 $O/brute.log; exit 1; }; tail -3 $O/brute.log; fi
+if [ -z "$NO_BRUTE" ]; then bash scripts/gpu/brute_pmc.sh ${BRUTE_TAG:-r5final} > $O/brute.log 2>&1 || { tail -5 $O/brute.log; exit 1; }; tail -3 $O/brute.log; fi
