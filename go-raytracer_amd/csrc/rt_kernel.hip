@@ -2694,10 +2694,16 @@ int rt_read_stats(rt_context* c, void* stream, int reset, rt_stats* out) {
       }
 #ifdef RT_CSG_DIAG
       {
-        unsigned long long cd[4] = {0, 0, 0, 0};
-        if (hipMemcpyFromSymbol(cd, HIP_SYMBOL(g_csg_diag), sizeof cd) == hipSuccess && cd[0])
+        unsigned long long cd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyFromSymbol(cd, HIP_SYMBOL(g_csg_diag), sizeof cd) == hipSuccess && cd[0]) {
           fprintf(stderr, "[csg] searches %llu, register-list overflows %llu (%.2f%%), mean live leaves %.2f\n", cd[0],
                   cd[1], 100.0 * cd[1] / cd[0], (double)cd[2] / cd[0]);
+          if (cd[6])
+            fprintf(stderr,
+                    "[csg] group visits %llu: leaf-major iterations %llu (lanes %.1f of 64), lane-major %llu (lanes "
+                    "%.1f), lane-leaf candidates %llu\n",
+                    cd[6], cd[3], cd[3] ? (double)cd[5] / cd[3] : 0.0, cd[4], cd[4] ? (double)cd[5] / cd[4] : 0.0, cd[5]);
+        }
       }
 #endif
       {

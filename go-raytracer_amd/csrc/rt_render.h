@@ -1143,7 +1143,7 @@ __device__ __forceinline__ bool csg_hit_all(DP geo, IP kinds, IP code, int nobj,
 }
 
 #ifdef RT_CSG_DIAG
-__device__ unsigned long long g_csg_diag[4];  // diagnostic build: searches, overflows, live leaves
+__device__ unsigned long long g_csg_diag[8];  // diagnostic build: searches, overflows, live leaves, group loop shapes
 #undef RT_CSG_DIAG
 #define RT_CSG_DIAG g_csg_diag
 #endif
@@ -1242,6 +1242,35 @@ __device__ __forceinline__ bool csg_hit(DP geo, IP kinds, IP code, int nobj,
       const bool gh = may_hit_s(true, of, df, 3.0e38f, __int_as_float(gr[0]), __int_as_float(gr[1]),
                                 __int_as_float(gr[2]), __int_as_float(gr[3]), slack);
       if (!wave_any(gh)) continue;
+#ifdef RT_CSG_DIAG
+      {
+        // the group's leaf loop as it runs (one iteration per leaf any lane
+        // may hit) vs lane-major (each lane its own next candidate: the most
+        // candidates one lane has), and the lane-leaf work both share
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane(gr[4]),
+                       d1 = (uint32_t)__builtin_amdgcn_readfirstlane(gr[5]);
+        int cand = 0, leaf_major = 0;
+        for (int e = 0; e < 8; e++) {
+          const int j = (int)(((e < 4 ? d0 : d1) >> (8 * (e & 3))) & 0xffu);
+          if (j == 0xff) break;
+          const int k = kinds[first + j];
+          const auto lg = geo + (size_t)(first + j) * GEO;
+          const bool pc = gh && (k == RT_PLANE || may_hit(of, df, 3.0e38f, lg, slack));
+          cand += pc ? 1 : 0;
+          leaf_major += wave_any(pc) ? 1 : 0;
+        }
+        int lane_major = 0;
+        for (int v = 0; v < 8; v++)
+          if (wave_any(cand > v)) lane_major = v + 1;
+        const int lid = (int)__lane_id();
+        if (__builtin_amdgcn_readfirstlane(lid) == lid) {
+          atomicAdd(RT_CSG_DIAG + 3, (unsigned long long)leaf_major);
+          atomicAdd(RT_CSG_DIAG + 4, (unsigned long long)lane_major);
+          atomicAdd(RT_CSG_DIAG + 6, 1ull);  // (wave, group) visits
+        }
+        atomicAdd(RT_CSG_DIAG + 5, (unsigned long long)cand);
+      }
+#endif
       if (gh) {
         const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane(gr[4]),
                        w1 = (uint32_t)__builtin_amdgcn_readfirstlane(gr[5]);
