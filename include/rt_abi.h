@@ -507,7 +507,10 @@ int rt_render(const rt_scene *scene, uint8_t *rgba_out, rt_stats *stats);
  * (no hipRTC); RT_RENDER_SPEC_SYNC -- a new scene shape waits for its
  * specialised kernel instead of rendering with the generic one meanwhile.
  * bands: row bands per device (0: one per ~2 M pixels of the share, <= 4;
- * RT_RENDER_BANDS in the environment overrides the automatic count).
+ * RT_RENDER_BANDS in the environment overrides the automatic count). Bands
+ * decrease in size (weights n, n-1, ..., 1; RT_RENDER_BAND_SHAPE=0: equal), so
+ * the exposed copy after the last band is the smallest band's. Environment
+ * knobs are read from the library's load-time copy of the environment.
  *
  * Kept per device between calls: two contexts with the last scene (an
  * unchanged scene -- byte-equal arrays -- is not converted, uploaded or
