@@ -1426,6 +1426,8 @@ int rt_spec_precompile(int nobj, const int* kinds, int features, double* compile
   return rc;
 }
 
+const char* rt_debug_getenv(const char* name) { return name ? rt_getenv(name) : nullptr; }
+
 int rt_debug_spec_compile(const char* key, double* compile_ms) {
   if (compile_ms) *compile_ms = 0;
   if (!key) return fail(RT_E_INVALID, "rt_debug_spec_compile: NULL key");

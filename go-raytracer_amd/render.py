@@ -89,6 +89,8 @@ def load_library(path=None):
     l.rt_debug_assemble.restype = i
     l.rt_debug_spec_compile.argtypes = [C.c_char_p, C.POINTER(C.c_double)]
     l.rt_debug_spec_compile.restype = i
+    l.rt_debug_getenv.argtypes = [C.c_char_p]
+    l.rt_debug_getenv.restype = C.c_char_p
     if l.rt_abi_version() != abi.RT_ABI_VERSION:
         raise RenderError("librtamd ABI version mismatch")
     _lib = l

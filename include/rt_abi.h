@@ -454,6 +454,13 @@ int rt_spec_precompile(int nobj, const int *kinds, int features, double *compile
  * this process), so a compiler abort is a failed compile, not a dead caller. */
 int rt_debug_spec_compile(const char *key, double *compile_ms);
 
+/* Diagnostic (tests, no device): the value of environment variable `name` as
+ * the library sees it -- its copy of the process environment taken when the
+ * library was loaded (every RT_* knob, the compile helper's environment and
+ * the in-process compiler's come from it; changes made after loading are not
+ * seen) -- or NULL. The string lives as long as the process. */
+const char *rt_debug_getenv(const char *name);
+
 /* Diagnostic (tests): run surface program `program` of the context's scene on
  * n (face, u, v) inputs on the device; out10 receives n x 10 Material fields
  * (rt_material order), err n flags (1 = the reference would raise). */
