@@ -1,5 +1,6 @@
 # Round 6: c4csg with CSG leaf groups of at most G leaves (RT_CSG_GROUP_LEAVES,
 # host-side grouping), interleaved rounds.
+# (the RT_CSG_GROUP_LEAVES knob was removed after this measurement: profiles/r06/csg_groups/)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
