@@ -446,6 +446,15 @@ int rt_render_ex(const rt_scene* scene, const rt_render_opts* opts, uint8_t* rgb
   const auto t0 = clk::now();
   auto ms_since = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   g_api_timing = rt_render_timing();
+  // RT_DEBUG_SEAM=1 (diagnostics): the setup steps of each call on stderr
+  static const bool dbg_seam = env_int("RT_DEBUG_SEAM", 0) != 0;
+  auto t_mark = t0;
+  auto mark = [&](const char* what) {
+    if (!dbg_seam) return;
+    const auto t = clk::now();
+    fprintf(stderr, "[seam] %-22s %8.3f ms\n", what, ms_since(t_mark, t));
+    t_mark = t;
+  };
   if (!scene || !rgba_out) return fail(RT_E_INVALID, "rt_render: NULL argument");
   if (scene->width <= 1 || scene->height <= 1) return fail(RT_E_INVALID, "rt_set_scene: width/height must be > 1");
   const int flags = opts ? opts->flags : 0;
@@ -490,6 +499,7 @@ int rt_render_ex(const rt_scene* scene, const rt_render_opts* opts, uint8_t* rgb
       slots.push_back(sl);
     }
   }
+  mark("slots");
   const int W = scene->width, H = scene->height;
   const ApiPlan plan = api_plan(W, H, N, opts ? opts->bands : 0);
   const size_t frame_bytes = (size_t)W * H * 4;
@@ -507,6 +517,7 @@ int rt_render_ex(const rt_scene* scene, const rt_render_opts* opts, uint8_t* rgb
     int rc = api_alloc_pinned(fr, frame_bytes);
     if (rc != RT_OK) return rc;
   }
+  mark("buffers");
   size_t stage_bytes = 0;
   std::vector<size_t> stage_off(N, 0);
   if (gather == RT_GATHER_PEER) {
@@ -538,6 +549,7 @@ int rt_render_ex(const rt_scene* scene, const rt_render_opts* opts, uint8_t* rgb
     if (rc != RT_OK) return rc;
   }
 
+  mark("peer gather setup");
   // scene: converted once when its bytes changed, cloned to every context
   std::vector<char> sb;
   scene_bytes(scene, sb);
@@ -580,6 +592,7 @@ int rt_render_ex(const rt_scene* scene, const rt_render_opts* opts, uint8_t* rgb
       slots[d]->spec = want_spec;
     }
   }
+  mark("scene set / clone");
   // reset counters a failed call may have left; the specialised variants the
   // bands will launch queued now (async compiles)
   for (int d = 0; d < N; d++) {
@@ -600,6 +613,7 @@ int rt_render_ex(const rt_scene* scene, const rt_render_opts* opts, uint8_t* rgb
     }
   }
 
+  mark("counters + prefetch");
   // launches: per slot its bands alternating over the two contexts / streams;
   // each band's copy queued behind it
   bool all_spec = true;
@@ -663,6 +677,7 @@ int rt_render_ex(const rt_scene* scene, const rt_render_opts* opts, uint8_t* rgb
     if (!out_dev) HIP_TRY(hipMemcpyAsync(fr.pinned, fr.frame, frame_bytes, hipMemcpyDeviceToHost, fr.gather));
     HIP_TRY(hipEventRecord(fr.gather_done, fr.gather));
   }
+  mark("launches");
   const auto t_launched = clk::now();
 
   // host side: finished bands copied on to rgba_out while later ones render
